@@ -1,0 +1,267 @@
+"""ORACLE — CPU restatement of the reference IK hot path. TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker (or the timed CPU baseline). The product
+path (temporal_inverse_kinematics_amd/) never imports it.
+
+Parity pinned: every function here is checked against golden vectors produced
+by the reference itself (tests/golden/make_golden.py → tests/golden/*.npz).
+
+numpy, float64 by default (dtype selectable), unfused, in the reference's own
+operation order. File:line citations are into /root/reference.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+
+BN_EPS = 1e-5          # torch.nn.BatchNorm{1,2}d default eps
+LEAKY_SLOPE = 0.01     # torch.nn.LeakyReLU default (pose_trainer.py:90)
+
+
+# ---------------------------------------------------------------- graph.py
+def _edges(layout: str):
+    """graph.py:38-85 (edge lists and centers)."""
+    if layout == "openpose":
+        n = 18
+        nb = [(4, 3), (3, 2), (7, 6), (6, 5), (13, 12), (12, 11), (10, 9), (9, 8), (11, 5),
+              (8, 2), (5, 1), (2, 1), (0, 1), (15, 0), (14, 0), (17, 15), (16, 14)]
+        return n, [(i, i) for i in range(n)] + nb, 1
+    if layout == "ntu-rgb+d":
+        n = 25
+        nb1 = [(1, 2), (2, 21), (3, 21), (4, 3), (5, 21), (6, 5), (7, 6), (8, 7), (9, 21),
+               (10, 9), (11, 10), (12, 11), (13, 1), (14, 13), (15, 14), (16, 15), (17, 1),
+               (18, 17), (19, 18), (20, 19), (22, 23), (23, 8), (24, 25), (25, 12)]
+        return n, [(i, i) for i in range(n)] + [(i - 1, j - 1) for i, j in nb1], 20
+    if layout == "ntu_edge":
+        n = 24
+        nb1 = [(1, 2), (3, 2), (4, 3), (5, 2), (6, 5), (7, 6), (8, 7), (9, 2), (10, 9),
+               (11, 10), (12, 11), (13, 1), (14, 13), (15, 14), (16, 15), (17, 1), (18, 17),
+               (19, 18), (20, 19), (21, 22), (22, 8), (23, 24), (24, 12)]
+        return n, [(i, i) for i in range(n)] + [(i - 1, j - 1) for i, j in nb1], 2
+    if layout == "coco":
+        n = 17
+        nb1 = [[16, 14], [14, 12], [17, 15], [15, 13], [12, 13], [6, 12], [7, 13], [6, 7],
+               [8, 6], [9, 7], [10, 8], [11, 9], [2, 3], [2, 1], [3, 1], [4, 2], [5, 3],
+               [4, 6], [5, 7]]
+        return n, [(i, i) for i in range(n)] + [(i - 1, j - 1) for i, j in nb1], 0
+    raise ValueError("Do Not Exist This Layout.")
+
+
+def hop_distance(n, edges, max_hop):
+    """graph.py:136-148 (inf for unreachable)."""
+    A = np.zeros((n, n))
+    for i, j in edges:
+        A[i, j] = A[j, i] = 1
+    hop = np.full((n, n), np.inf)
+    reach = [np.linalg.matrix_power(A, d) > 0 for d in range(max_hop + 1)]
+    for d in range(max_hop, -1, -1):
+        hop[reach[d]] = d
+    return hop
+
+
+def graph_A(layout="coco", strategy="uniform", max_hop=1, dilation=1) -> np.ndarray:
+    """Graph(...).A, graph.py:25-37,91-133 with normalize_digraph graph.py:151-159."""
+    n, edges, center = _edges(layout)
+    hop = hop_distance(n, edges, max_hop)
+    valid = range(0, max_hop + 1, dilation)
+    adj = np.zeros((n, n))
+    for h in valid:
+        adj[hop == h] = 1
+    dl = adj.sum(0)
+    dn = np.diag(np.where(dl > 0, 1.0 / np.where(dl > 0, dl, 1), 0.0))
+    norm = adj @ dn
+    if strategy == "uniform":
+        return norm[None]
+    if strategy == "distance":
+        A = np.zeros((len(valid), n, n))
+        for i, h in enumerate(valid):
+            A[i][hop == h] = norm[hop == h]
+        return A
+    if strategy == "spatial":
+        out = []
+        for h in valid:
+            root = np.zeros((n, n)); close = np.zeros((n, n)); far = np.zeros((n, n))
+            for i in range(n):
+                for j in range(n):
+                    if hop[j, i] == h:
+                        if hop[j, center] == hop[i, center]:
+                            root[j, i] = norm[j, i]
+                        elif hop[j, center] > hop[i, center]:
+                            close[j, i] = norm[j, i]
+                        else:
+                            far[j, i] = norm[j, i]
+            if h == 0:
+                out.append(root)
+            else:
+                out.append(root + close)
+                out.append(far)
+        return np.stack(out)
+    raise ValueError("Do Not Exist This Strategy")
+
+
+# ---------------------------------------------------------------- layers
+def batchnorm(x, p: Dict[str, np.ndarray], prefix: str, axis: int = 1):
+    """Eval-mode BatchNorm (running stats), channel on `axis`."""
+    shape = [1] * x.ndim
+    shape[axis] = -1
+    g = p[prefix + ".weight"].astype(x.dtype).reshape(shape)
+    b = p[prefix + ".bias"].astype(x.dtype).reshape(shape)
+    m = p[prefix + ".running_mean"].astype(x.dtype).reshape(shape)
+    v = p[prefix + ".running_var"].astype(x.dtype).reshape(shape)
+    return (x - m) / np.sqrt(v + BN_EPS) * g + b
+
+
+def conv_t(x, w, b, stride=1, padding=0, dilation=1):
+    """Conv2d with kernel (kt,1) on (N,C,T,V) — the only conv shape the path uses
+    (gconv_origin.py:49-55, st_gcn_aaai18.py:180-186,199-202)."""
+    N, C, T, V = x.shape
+    Co, Ci, kt, _ = w.shape
+    assert Ci == C
+    xp = np.pad(x, ((0, 0), (0, 0), (padding, padding), (0, 0)))
+    To = (T + 2 * padding - dilation * (kt - 1) - 1) // stride + 1
+    out = np.zeros((N, Co, To, V), dtype=x.dtype)
+    for k in range(kt):
+        sl = xp[:, :, k * dilation: k * dilation + stride * (To - 1) + 1: stride, :]
+        out += np.einsum("oc,nctv->notv", w[:, :, k, 0].astype(x.dtype), sl, optimize=True)
+    if b is not None:
+        out += b.astype(x.dtype)[None, :, None, None]
+    return out
+
+
+def gconv(x, A, w, b, K, t_stride=1, t_padding=0, t_dilation=1):
+    """ConvTemporalGraphical.forward, gconv_origin.py:56-65."""
+    assert A.shape[0] == K
+    y = conv_t(x, w, b, t_stride, t_padding, t_dilation)
+    n, kc, t, v = y.shape
+    y = y.reshape(n, K, kc // K, t, v)
+    return np.einsum("nkctv,kvw->nctw", y, A.astype(x.dtype), optimize=True)
+
+
+def stgcn_block(x, A, p: Dict[str, np.ndarray], prefix: str, cin, cout, stride, residual=True, kt=3):
+    """StGcnBlock.forward, st_gcn_aaai18.py:208-214 (eval; Dropout p=0)."""
+    if not residual:
+        res = 0.0
+    elif cin == cout and stride == 1:
+        res = x
+    else:
+        res = conv_t(x, p[prefix + "residual.0.weight"], p[prefix + "residual.0.bias"], stride)
+        res = batchnorm(res, p, prefix + "residual.1")
+    y = gconv(x, A, p[prefix + "gcn.conv.weight"], p[prefix + "gcn.conv.bias"], A.shape[0])
+    y = np.maximum(batchnorm(y, p, prefix + "tcn.0"), 0)
+    y = conv_t(y, p[prefix + "tcn.2.weight"], p[prefix + "tcn.2.bias"], stride, (kt - 1) // 2)
+    y = batchnorm(y, p, prefix + "tcn.3")
+    return np.maximum(y + res, 0)
+
+
+IK_LAYERS = [(3, 64, 1), (64, 64, 1), (64, 128, 2), (128, 128, 1),
+             (128, 128, 1), (128, 128, 2), (128, 256, 2), (256, 256, 2)]   # pose_trainer.py:76-83
+
+
+def backbone(x, p: Dict[str, np.ndarray], dtype=np.float64, layers=IK_LAYERS):
+    """StgGcn18.forward, st_gcn_aaai18.py:113-133. x: (N,T,V,C) -> (N,T',V*C')."""
+    x = np.asarray(x, dtype=dtype)
+    N, T, V, C = x.shape
+    h = x.transpose(0, 2, 3, 1).reshape(N, V * C, T)                  # :120-121
+    h = batchnorm(h, p, "backbone.data_bn", axis=1)                    # :122
+    h = h.reshape(N, V, C, T).transpose(0, 2, 3, 1)                    # :123-125 -> (N,C,T,V)
+    A = p["backbone.A"].astype(dtype)
+    for l, (ci, co, s) in enumerate(layers):                           # :128-129
+        Ae = A * p[f"backbone.edge_importance.{l}"].astype(dtype)
+        h = stgcn_block(h, Ae, p, f"backbone.st_gcn_networks.{l}.", ci, co, s)
+    h = h.transpose(0, 2, 3, 1)                                        # :131
+    return h.reshape(h.shape[0], h.shape[1], -1)                       # :132
+
+
+def head(feat, p, dtype=np.float64):
+    """pose_regressor, pose_trainer.py:89-92,103-106 (Dropout eval = identity)."""
+    f = np.asarray(feat, dtype=dtype)
+    h = f @ p["pose_regressor.0.weight"].astype(dtype).T + p["pose_regressor.0.bias"].astype(dtype)
+    h = np.where(h > 0, h, LEAKY_SLOPE * h)
+    return h @ p["pose_regressor.3.weight"].astype(dtype).T + p["pose_regressor.3.bias"].astype(dtype)
+
+
+def pose_regressor(x, p, dtype=np.float64) -> Dict[str, np.ndarray]:
+    """PoseRegressor.forward, pose_trainer.py:94-133 -> {'poses': (N,T',66)}."""
+    feat = backbone(x, p, dtype)
+    n, w, c = feat.shape
+    y = head(feat.reshape(n * w, c), p, dtype)
+    return {"poses": y.reshape(n, w, -1)}
+
+
+# ---------------------------------------------------------------- windowing
+def sample_window(arr, idx, h):
+    """data_amass.py:18-42 (edge padding; its ValueError condition kept verbatim)."""
+    F = arr.shape[0]
+    pad_l = pad_r = 0
+    if h > idx > F - h:
+        raise ValueError(f"h_win_size > idx > arr.shape[0] - h_win_size: {h} > {idx} > {F} - {h}")
+    elif idx < h:
+        pad_l = h - idx
+    elif idx > F - h - 1:
+        pad_r = idx - (F - h) + 1
+    # frames of the edge-padded array, sliced [idx+pad_l-h, idx+pad_l+h+1): the
+    # slice can run past the padded end (short sequences), as in the reference
+    lo, hi = idx + pad_l - h, min(idx + pad_l + h + 1, F + pad_l + pad_r)
+    frames = np.clip(np.arange(lo, hi) - pad_l, 0, F - 1)
+    return arr[frames]
+
+
+def inference_item(seq, idx, win_size, relative=True):
+    """InferenceDataset.__getitem__, data_amass.py:230-236."""
+    w = sample_window(seq, idx, win_size // 2)
+    if relative:
+        root = 0.5 * (w[:, 11, :] + w[:, 12, :])
+        w = w - root[:, None, :]
+    return w
+
+
+def run_inference(seq, p, win_size, batch=64, dtype=np.float64):
+    """inference.run_inference, inference.py:37-67 (keeps window output frame 0)."""
+    F = seq.shape[0]
+    out = np.zeros((F, 66), dtype=np.float64)
+    for s in range(0, F, batch):
+        xs = np.stack([inference_item(seq, i, win_size) for i in range(s, min(F, s + batch))])
+        out[s:s + len(xs)] = pose_regressor(xs, p, dtype)["poses"][:, 0]
+    return out
+
+
+# ---------------------------------------------------------------- keypoints
+MOVEAI_TO_COCO = [-1, -1, -1, 20, 21, 11, 15, 12, 16, 13, 17, 5, 1, 6, 2, 7, 3]
+
+
+def moveai_to_coco(mv):
+    """keypoints_util.py:27-60 + inference.py:121-133 (head points, (x,z,-y))."""
+    out = np.zeros((mv.shape[0], 17, 3), dtype=np.float32)
+    for t, s in enumerate(MOVEAI_TO_COCO):
+        if s >= 0:
+            out[:, t] = mv[:, s]
+    out[:, 0] = 0.5 * (mv[:, -1] + mv[:, -2])
+    out[:, 1] = mv[:, -2]
+    out[:, 2] = mv[:, -1]
+    y = out[:, :, 1].copy()
+    out[:, :, 1] = out[:, :, 2]
+    out[:, :, 2] = -y
+    return out
+
+
+# ---------------------------------------------------------------- rotations
+def angle_axis_to_rotation_matrix(aa, dtype=np.float64):
+    """kornia_geometry_conversion.py:125-201: Rodrigues with w = aa/(theta+1e-6)
+    when theta^2 > 1e-6, else the first-order Taylor form."""
+    aa = np.asarray(aa, dtype=dtype)
+    th2 = (aa * aa).sum(-1)
+    th = np.sqrt(th2)
+    w = aa / (th + 1e-6)[:, None]
+    wx, wy, wz = w[:, 0], w[:, 1], w[:, 2]
+    c, s = np.cos(th), np.sin(th)
+    oc = 1.0 - c
+    Rn = np.stack([c + wx * wx * oc, wx * wy * oc - wz * s, wy * s + wx * wz * oc,
+                   wz * s + wx * wy * oc, c + wy * wy * oc, -wx * s + wy * wz * oc,
+                   -wy * s + wx * wz * oc, wx * s + wy * wz * oc, c + wz * wz * oc], -1)
+    rx, ry, rz = aa[:, 0], aa[:, 1], aa[:, 2]
+    one = np.ones_like(rx)
+    Rt = np.stack([one, -rz, ry, rz, one, -rx, -ry, rx, one], -1)
+    R = np.where((th2 > 1e-6)[:, None], Rn, Rt)
+    return R.reshape(-1, 3, 3)

@@ -1,0 +1,179 @@
+"""Headline benchmark: IK frames/s (COCO-17 -> SMPL-X body pose) on MI355X.
+
+One step = one fused IK forward of the rank's batch of B=1024 synthetic
+AMASS-shaped windows (T=64, inputs already resident in HBM), and for N>1 the
+RCCL all-gather of the (B,T',66) pose parameters to every rank over xGMI
+(BASELINE.json config #2 at N=1, config #3 = 8x1024 at N=8; weak scaling).
+IK frame := one window -> one solved frame (inference.py:58-64).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--T T]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line with the metric, the roofline of the dominant
+kernel (HIP events around its launches inside the timed region) and a CPU
+baseline (the oracle, fixture-pinned to the reference, on host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-in MFMA (= f32 vector) peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
+
+
+def _cpu_baseline(T: int, seconds: float = 12.0):
+    """Oracle (numpy fp32, the reference algorithm unfused) on a bounded sample."""
+    import numpy as np
+    from threadpoolctl import threadpool_info
+
+    from oracle import stgcn as orc
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
+    nb = 8
+    x = syn.synthetic_windows(nb, T, seed=7)
+    orc.pose_regressor(x[:1], sd, dtype=np.float32)     # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.pose_regressor(x, sd, dtype=np.float32)
+        done += nb
+    dt = time.perf_counter() - t0
+    threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    return {"value": done / dt, "unit": "IK frames/s", "cores": int(threads), "kind": "port",
+            "sample": f"{done} windows (T={T}) of the numpy fp32 oracle (oracle/stgcn.py, pinned to the "
+                      f"reference's fixtures) in {dt:.1f}s on {os.cpu_count()} visible host CPUs"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="windows per GPU")
+    ap.add_argument("--T", type=int, default=64, help="frames per window")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0 and world > 1:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from temporal_inverse_kinematics_amd import _build, _lib, synthetic as syn
+    from temporal_inverse_kinematics_amd.distributed import gather_poses
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    if rank == 0:
+        _build.build()
+    if world > 1:
+        dist.barrier()
+
+    B, T = args.batch, args.T
+    model = synthetic_model(win_size=T, device=dev)
+    reg = model.regressor
+    x = torch.from_numpy(syn.synthetic_windows(B, T, seed=0, start=rank * B)).to(dev)
+    Tp = reg.backbone.out_frames(T)
+    full = torch.empty((world * B, Tp, 66), device=dev) if world > 1 else None
+
+    def step():
+        y = reg(x)["poses"]
+        if world > 1:
+            gather_poses(y, full)
+        return y
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        lib = _lib.load()
+        h = reg.tik_handle()
+        per_fwd = 2 * len(reg.backbone.st_gcn_networks) + 3
+        _lib.check(lib.tik_model_profile(h, per_fwd * args.steps))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+
+        # per-kernel HIP-event timings from the timed region
+        n = _lib.check(lib.tik_model_profile_count(h))
+        agg = {}
+        lab = ctypes.create_string_buffer(64)
+        ms, fl, by = ctypes.c_float(), ctypes.c_double(), ctypes.c_double()
+        for i in range(n):
+            _lib.check(lib.tik_model_profile_read(h, i, lab, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by)))
+            kern = lab.value.decode().split(".")[0]
+            a = agg.setdefault(kern, [0.0, 0, 0.0, 0.0])
+            a[0] += ms.value; a[1] += 1; a[2] += fl.value; a[3] += by.value
+        lib.tik_model_profile(h, 0)
+
+    ms_step = dt / args.steps * 1e3
+    value = world * B / (dt / args.steps)
+    if rank == 0:
+        dom = max(agg, key=lambda k: agg[k][0])
+        tot_ms, cnt, tot_fl, tot_by = agg[dom]
+        avg_s = tot_ms / cnt / 1e3
+        achieved = tot_fl / cnt / avg_s / 1e12
+        kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
+                       "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 2), "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1)}
+                   for k, v in agg.items()}
+        fwd_flops = sum(v[2] for v in agg.values()) / args.steps
+        out = {
+            "metric": "IK frames/sec (COCO-17->SMPLx pose)",
+            "value": round(value, 1),
+            "unit": "IK frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (AMASS-shaped windows from the sample sequence; seeded synthetic weights)",
+            "config": {"workload": f"ST-GCN IK forward, batch={B}x{T}-frame x COCO-17 windows per GPU -> (B,{Tp},66) "
+                                   f"SMPL-X pose" + (f", RCCL all-gather of poses over {world} GPUs" if world > 1 else ""),
+                       "global_batch": world * B, "window_frames": T, "out_frames": Tp,
+                       "parallelism": f"dp{world}" if world > 1 else "single"},
+            "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": None,
+                         "hbm_gbs_algorithmic": round(tot_by / cnt / avg_s / 1e9, 1),
+                         "hbm_frac_algorithmic": round(tot_by / cnt / avg_s / 1e9 / HBM_PEAK_GBS, 5)},
+            "forward": {"algorithmic_tflops": round(fwd_flops * args.steps / dt / 1e12, 2),
+                        "mflop_per_window": round(fwd_flops / B / 1e6, 2), "kernels": kernels},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = _cpu_baseline(T, args.cpu_seconds)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+/*
+ * tik.h — C ABI of libtik.so, the MI355X-native temporal-IK engine.
+ *
+ * Every compute entry point takes caller-owned DEVICE pointers (fp32,
+ * row-major, explicit dims) and a hipStream_t passed as `void*` (NULL = the
+ * legacy default stream), is stream-ordered, and returns an int status:
+ * TIK_OK (0) or a negative TIK_E_* code; tik_last_error() returns the text of
+ * the calling thread's last failure. Handles own their device weights and
+ * workspace; per-call functions allocate only through the handle. Calls are
+ * thread-safe across distinct handles/streams.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repository root).
+ */
+#ifndef TIK_H
+#define TIK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TIK_OK 0
+#define TIK_E_INVALID (-1)   /* bad argument / shape: Python raises ValueError  */
+#define TIK_E_HIP (-2)       /* HIP runtime error: Python raises RuntimeError   */
+#define TIK_E_MISSING (-3)   /* missing state-dict tensor: Python raises KeyError */
+#define TIK_E_NOMEM (-4)     /* device allocation failed                        */
+
+typedef struct tik_model* tik_model_t;
+typedef struct tik_fk* tik_fk_t;
+
+/* One named host fp32 tensor of a state dict (weight ABI = reference keys). */
+typedef struct {
+    const char* name;      /* e.g. "backbone.st_gcn_networks.3.tcn.2.weight" */
+    const float* data;     /* host pointer, contiguous                        */
+    int ndim;
+    int64_t shape[4];
+} tik_tensor;
+
+const char* tik_last_error(void);
+const char* tik_version(void);
+
+/* ------------------------------------------------------------------------
+ * IK model: PoseRegressor = StgGcn18 backbone + MLP head.
+ * Replaces pose_trainer.py:66-133 (PoseRegressor.__init__/forward) and
+ * IKPoseTrainer.forward pose_trainer.py:143-144, as called by
+ * inference.run_inference inference.py:51.
+ *
+ * tik_model_create: `tensors` is the PoseRegressor state dict (keys without
+ * the Lightning "regressor." prefix; num_batches_tracked ignored). Layer
+ * shapes are inferred from the tensors (pose_trainer.py:76-83 config).
+ * BatchNorm (eval) is folded into the convolutions on the host, then the
+ * packed weights are uploaded once.
+ * ---------------------------------------------------------------------- */
+int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out);
+int tik_model_destroy(tik_model_t m);
+/* Output frames T' for an input window of T frames (4 stride-2 layers). */
+int tik_model_out_frames(tik_model_t m, int T);
+/* Grow the handle-owned workspace for batches up to (N,T); optional. */
+int tik_model_reserve(tik_model_t m, int N, int T);
+/* keypoints x: (N,T,V=17,C=3) fp32 device; poses: (N,T',66) fp32 device. */
+int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream);
+/* Backbone only (StgGcn18.forward, st_gcn_aaai18.py:113-133): feat (N,T',V*Cout). */
+int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream);
+
+/* Per-launch HIP-event profiling of the model's kernels (used by bench.py):
+ * tik_model_profile(m, n) records up to n launches (0 disables, clears);
+ * after synchronising, tik_model_profile_read returns launch i's label
+ * ("<tile config>.<role>"), elapsed ms, and algorithmic FLOPs / bytes. */
+int tik_model_profile(tik_model_t m, int max_launches);
+int tik_model_profile_count(tik_model_t m);
+int tik_model_profile_read(tik_model_t m, int i, char* label, int label_len, float* ms, double* flops,
+                           double* bytes);
+
+/* ------------------------------------------------------------------------
+ * One StGcnBlock (st_gcn_aaai18.py:136-214, eval mode) on channels-last data.
+ * x: (N,T,V,Cin) device, out: (N,T',V,Cout) device, A_eff: (V,V) device
+ * (= A * edge_importance, st_gcn_aaai18.py:129), K = 1 (uniform strategy).
+ * `tensors` is the block's state dict (keys "gcn.conv.weight", "tcn.0.*",
+ * "tcn.2.*", "tcn.3.*", "residual.0.*", "residual.1.*").
+ * residual: 0 = none (zero), 1 = module default (iden or conv per :191-204).
+ * ---------------------------------------------------------------------- */
+typedef struct tik_block* tik_block_t;
+int tik_block_create(const tik_tensor* tensors, int n_tensors, int in_channels, int out_channels,
+                     int stride, int residual, const float* A_eff_host, int V, tik_block_t* out);
+int tik_block_destroy(tik_block_t b);
+int tik_stgcn_block_fwd(tik_block_t b, const float* x, int N, int T, float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * ConvTemporalGraphical.forward (gconv_origin.py:56-65), reference layout.
+ * x (N,Cin,T,V), A (K,V,V), W (K*Cout, Cin, t_kernel, 1), b (K*Cout) or NULL,
+ * out (N,Cout,T_out,V) with T_out = (T + 2p - d*(tk-1) - 1)/s + 1. All device.
+ * ---------------------------------------------------------------------- */
+int tik_gconv_fwd(const float* x, int N, int Cin, int T, int V, const float* A, int K,
+                  const float* W, const float* b, int Cout, int t_kernel, int t_stride,
+                  int t_padding, int t_dilation, float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * kornia angle_axis_to_rotation_matrix (common/kornia_geometry_conversion.py:125-201):
+ * aa (n,3) -> R (n,3,3), device pointers.
+ * ---------------------------------------------------------------------- */
+int tik_aa_to_rotmat(const float* aa, int n, float* R, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Windowing (mmskeleton/datasets/data_amass.py:18-42 sample_window and
+ * :221-236 InferenceDataset, relative_pose=True) on the device:
+ * seq (F,V,3) -> windows (n_idx, 2h+1, V, 3) for centre frames
+ * idx0 .. idx0+n_idx-1, edge-padded, root-relative (root = mean of joints
+ * root_a, root_b; COCO 11/12). Returns TIK_E_INVALID when any requested
+ * window would raise ValueError or be short in the reference.
+ * ---------------------------------------------------------------------- */
+int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h, int root_a,
+                      int root_b, int relative, float* windows, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TIK_H */

@@ -115,19 +115,20 @@ def batchnorm(x, p: Dict[str, np.ndarray], prefix: str, axis: int = 1):
 
 def conv_t(x, w, b, stride=1, padding=0, dilation=1):
     """Conv2d with kernel (kt,1) on (N,C,T,V) — the only conv shape the path uses
-    (gconv_origin.py:49-55, st_gcn_aaai18.py:180-186,199-202)."""
+    (gconv_origin.py:49-55, st_gcn_aaai18.py:180-186,199-202). One BLAS GEMM per tap."""
     N, C, T, V = x.shape
     Co, Ci, kt, _ = w.shape
     assert Ci == C
     xp = np.pad(x, ((0, 0), (0, 0), (padding, padding), (0, 0)))
     To = (T + 2 * padding - dilation * (kt - 1) - 1) // stride + 1
-    out = np.zeros((N, Co, To, V), dtype=x.dtype)
+    xl = np.ascontiguousarray(xp.transpose(0, 2, 3, 1))            # (N, Tp, V, C)
+    out = np.zeros((N, To, V, Co), dtype=x.dtype)
     for k in range(kt):
-        sl = xp[:, :, k * dilation: k * dilation + stride * (To - 1) + 1: stride, :]
-        out += np.einsum("oc,nctv->notv", w[:, :, k, 0].astype(x.dtype), sl, optimize=True)
+        sl = xl[:, k * dilation: k * dilation + stride * (To - 1) + 1: stride]
+        out += (sl.reshape(-1, C) @ w[:, :, k, 0].astype(x.dtype).T).reshape(N, To, V, Co)
     if b is not None:
-        out += b.astype(x.dtype)[None, :, None, None]
-    return out
+        out += b.astype(x.dtype)
+    return out.transpose(0, 3, 1, 2)
 
 
 def gconv(x, A, w, b, K, t_stride=1, t_padding=0, t_dilation=1):
@@ -136,7 +137,8 @@ def gconv(x, A, w, b, K, t_stride=1, t_padding=0, t_dilation=1):
     y = conv_t(x, w, b, t_stride, t_padding, t_dilation)
     n, kc, t, v = y.shape
     y = y.reshape(n, K, kc // K, t, v)
-    return np.einsum("nkctv,kvw->nctw", y, A.astype(x.dtype), optimize=True)
+    # einsum('nkctv,kvw->nctw') as a sum of per-k GEMMs over v
+    return sum(y[:, k] @ A[k].astype(x.dtype) for k in range(K))
 
 
 def stgcn_block(x, A, p: Dict[str, np.ndarray], prefix: str, cin, cout, stride, residual=True, kt=3):

@@ -1,0 +1,71 @@
+"""Build libtik.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension).
+
+    python -m temporal_inverse_kinematics_amd._build [--debug]
+
+The shared library lands next to this file (git-ignored, but it travels to
+the GPU box with the gpurun snapshot).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+REPO = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "libtik.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _needs_rebuild(objs_srcs, lib):
+    if not os.path.exists(lib):
+        return True
+    t = os.path.getmtime(lib)
+    deps = _sources() + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(REPO, "include", "tik.h"),
+                                                                 os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force: bool = False, debug: bool = False, verbose: bool = False) -> str:
+    srcs = _sources()
+    objdir = os.path.join(PKG, "build")
+    os.makedirs(objdir, exist_ok=True)
+    if not force and not _needs_rebuild(srcs, LIB):
+        return LIB
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
+              f"-I{os.path.join(REPO, 'include')}", *opt]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = common + ["-c", src, "-o", obj]
+        if src.endswith(".cpp"):
+            cmd = common + ["-x", "hip", "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")
+        if verbose and (r.stderr or r.stdout):
+            print(r.stdout + r.stderr)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = LIB + ".tmp"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, debug="--debug" in sys.argv, verbose=True))

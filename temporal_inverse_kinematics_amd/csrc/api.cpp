@@ -1,0 +1,573 @@
+// api.cpp — the C ABI of libtik.so (include/tik.h): weight folding/packing,
+// handle-owned workspace, and the launch sequence of the IK forward pass.
+//
+// Forward of PoseRegressor (pose_trainer.py:94-133) on channels-last data:
+//   xb  = data_bn(x)                                      st_gcn_aaai18.py:119-125
+//   per block l (st_gcn_aaai18.py:208-214):
+//     z   = ReLU( mix_A( x . Wg'^T ) + bias2[w][c] )      gcn + tcn.0 BN + ReLU (folded)
+//     out = ReLU( sum_tap z[s t'+tap-1] . Wt'_tap^T + res + bT )   tcn.2 + tcn.3 BN + residual
+//   feat = out_7 viewed (N*T', 17*256)                    st_gcn_aaai18.py:131-132
+//   poses = (LeakyReLU(feat . W0^T + b0)) . W3^T + b3      pose_trainer.py:89-92
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/tik.h"
+#include "cgemm.h"
+#include "misc.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(TIK_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr float BN_EPS = 1e-5f;
+constexpr int TK = 3;   // temporal kernel (pose_trainer.py:85)
+
+struct HostTensor {
+    std::vector<float> v;
+    std::vector<int64_t> shape;
+};
+
+using TensorMap = std::map<std::string, HostTensor>;
+
+TensorMap to_map(const tik_tensor* t, int n) {
+    TensorMap m;
+    for (int i = 0; i < n; ++i) {
+        if (!t[i].name) continue;
+        HostTensor h;
+        int64_t numel = 1;
+        for (int d = 0; d < t[i].ndim; ++d) {
+            h.shape.push_back(t[i].shape[d]);
+            numel *= t[i].shape[d];
+        }
+        if (t[i].data) h.v.assign(t[i].data, t[i].data + numel);
+        m[t[i].name] = std::move(h);
+    }
+    return m;
+}
+
+const HostTensor* find(const TensorMap& m, const std::string& k) {
+    auto it = m.find(k);
+    return it == m.end() ? nullptr : &it->second;
+}
+
+struct DevBuf {
+    float* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    int upload(const std::vector<float>& h) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = h.size();
+        if (n == 0) return TIK_OK;
+        if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return fail(TIK_E_NOMEM, "hipMalloc(%zu floats) failed", n);
+        if (hipMemcpy(p, h.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(TIK_E_HIP, "hipMemcpy H2D failed");
+        return TIK_OK;
+    }
+    int reserve(size_t want) {
+        if (want <= n) return TIK_OK;
+        if (p) { (void)hipFree(p); p = nullptr; }
+        if (hipMalloc(&p, want * sizeof(float)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu floats) failed", want); }
+        n = want;
+        return TIK_OK;
+    }
+};
+
+int round4(int c) { return (c + 3) & ~3; }
+
+// eval BatchNorm -> (scale, shift)
+int bn_fold(const TensorMap& m, const std::string& pre, int C, std::vector<float>& sc, std::vector<float>& sh) {
+    const HostTensor* g = find(m, pre + ".weight");
+    const HostTensor* b = find(m, pre + ".bias");
+    const HostTensor* mu = find(m, pre + ".running_mean");
+    const HostTensor* var = find(m, pre + ".running_var");
+    if (!g || !b || !mu || !var) return fail(TIK_E_MISSING, "missing BatchNorm tensors under '%s'", pre.c_str());
+    if ((int)g->v.size() != C || (int)b->v.size() != C || (int)mu->v.size() != C || (int)var->v.size() != C)
+        return fail(TIK_E_INVALID, "BatchNorm '%s' expects %d channels", pre.c_str(), C);
+    sc.resize(C);
+    sh.resize(C);
+    for (int c = 0; c < C; ++c) {
+        const double s = (double)g->v[c] / std::sqrt((double)var->v[c] + (double)BN_EPS);
+        sc[c] = (float)s;
+        sh[c] = (float)((double)b->v[c] - (double)mu->v[c] * s);
+    }
+    return TIK_OK;
+}
+
+enum ResKind { RES_ZERO = 0, RES_IDEN = 1, RES_CONV = 2 };
+
+// Optional per-launch HIP-event profiler (bench.py's roofline numbers): one
+// event pair per kernel launch on the launch stream, algorithmic FLOPs and
+// bytes computed from the shapes.
+struct Profiler {
+    struct Rec {
+        std::string label;
+        double flops, bytes;
+    };
+    std::vector<hipEvent_t> ev0, ev1;
+    std::vector<Rec> recs;
+    int cap = 0;
+    ~Profiler() { clear(); }
+    void clear() {
+        for (auto e : ev0) (void)hipEventDestroy(e);
+        for (auto e : ev1) (void)hipEventDestroy(e);
+        ev0.clear(); ev1.clear(); recs.clear(); cap = 0;
+    }
+    int enable(int n) {
+        clear();
+        for (int i = 0; i < n; ++i) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+                return fail(TIK_E_HIP, "hipEventCreate failed");
+            ev0.push_back(a); ev1.push_back(b);
+        }
+        cap = n;
+        return TIK_OK;
+    }
+    int begin(const char* label, double flops, double bytes, hipStream_t st) {
+        if ((int)recs.size() >= cap) return -1;
+        const int i = (int)recs.size();
+        recs.push_back({label, flops, bytes});
+        (void)hipEventRecord(ev0[i], st);
+        return i;
+    }
+    void end(int i, hipStream_t st) {
+        if (i >= 0) (void)hipEventRecord(ev1[i], st);
+    }
+};
+thread_local Profiler* g_prof = nullptr;   // set for the duration of a profiled call
+
+struct ProfScope {
+    int i;
+    hipStream_t st;
+    ProfScope(const char* label, double flops, double bytes, hipStream_t s) : st(s) {
+        i = g_prof ? g_prof->begin(label, flops, bytes, s) : -1;
+    }
+    ~ProfScope() { if (g_prof) g_prof->end(i, st); }
+};
+
+// One StGcnBlock with BN folded into packed fp32 weights.
+struct Layer {
+    int cin = 0, cinp = 0, cout = 0, stride = 1, res = RES_IDEN, V = 17;
+    DevBuf wg;      // [cout][cinp]          gcn conv scaled by tcn.0 BN
+    DevBuf bias2;   // [V][cout]             sc1*bg*colsum(A)[w] + sh1
+    DevBuf amix;    // [V][V]                A_eff[v][w]
+    DevBuf wt;      // [cout][3*cout]        tcn conv scaled by tcn.3 BN, k = tap*cout + ci
+    DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
+    DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
+
+    int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
+              const std::vector<float>& A_eff, int V_) {
+        cin = cin_; cout = cout_; stride = stride_; V = V_;
+        cinp = round4(cin);
+        if (cout % 4 != 0) return fail(TIK_E_INVALID, "out_channels must be a multiple of 4 (got %d)", cout);
+        res = !residual ? RES_ZERO : ((cin == cout && stride == 1) ? RES_IDEN : RES_CONV);
+        const HostTensor* Wg = find(m, pre + "gcn.conv.weight");
+        const HostTensor* bg = find(m, pre + "gcn.conv.bias");
+        if (!Wg) return fail(TIK_E_MISSING, "missing '%sgcn.conv.weight'", pre.c_str());
+        if ((int64_t)Wg->v.size() != (int64_t)cout * cin)
+            return fail(TIK_E_INVALID, "'%sgcn.conv.weight' must be (%d,%d,1,1) (spatial kernel K=1 only)", pre.c_str(), cout, cin);
+        std::vector<float> sc1, sh1, sc2, sh2;
+        int rc;
+        if ((rc = bn_fold(m, pre + "tcn.0", cout, sc1, sh1))) return rc;
+        if ((rc = bn_fold(m, pre + "tcn.3", cout, sc2, sh2))) return rc;
+        std::vector<double> colsum(V, 0.0);
+        for (int v = 0; v < V; ++v)
+            for (int w = 0; w < V; ++w) colsum[w] += A_eff[v * V + w];
+        std::vector<float> hwg((size_t)cout * cinp, 0.f), hb2((size_t)V * cout);
+        for (int co = 0; co < cout; ++co)
+            for (int ci = 0; ci < cin; ++ci) hwg[(size_t)co * cinp + ci] = sc1[co] * Wg->v[(size_t)co * cin + ci];
+        for (int w = 0; w < V; ++w)
+            for (int co = 0; co < cout; ++co) {
+                const double b = bg ? bg->v[co] : 0.0;
+                hb2[(size_t)w * cout + co] = (float)((double)sc1[co] * b * colsum[w] + sh1[co]);
+            }
+        const HostTensor* Wt = find(m, pre + "tcn.2.weight");
+        const HostTensor* bt = find(m, pre + "tcn.2.bias");
+        if (!Wt) return fail(TIK_E_MISSING, "missing '%stcn.2.weight'", pre.c_str());
+        if ((int64_t)Wt->v.size() != (int64_t)cout * cout * TK)
+            return fail(TIK_E_INVALID, "'%stcn.2.weight' must be (%d,%d,3,1)", pre.c_str(), cout, cout);
+        std::vector<float> hwt((size_t)cout * TK * cout), hbt(cout);
+        for (int co = 0; co < cout; ++co) {
+            for (int tap = 0; tap < TK; ++tap)
+                for (int ci = 0; ci < cout; ++ci)
+                    hwt[(size_t)co * TK * cout + tap * cout + ci] = sc2[co] * Wt->v[((size_t)co * cout + ci) * TK + tap];
+            hbt[co] = (float)((double)sc2[co] * (bt ? bt->v[co] : 0.0) + sh2[co]);
+        }
+        if (res == RES_CONV) {
+            const HostTensor* Wr = find(m, pre + "residual.0.weight");
+            const HostTensor* br = find(m, pre + "residual.0.bias");
+            if (!Wr) return fail(TIK_E_MISSING, "missing '%sresidual.0.weight'", pre.c_str());
+            if ((int64_t)Wr->v.size() != (int64_t)cout * cin)
+                return fail(TIK_E_INVALID, "'%sresidual.0.weight' must be (%d,%d,1,1)", pre.c_str(), cout, cin);
+            std::vector<float> scr, shr;
+            if ((rc = bn_fold(m, pre + "residual.1", cout, scr, shr))) return rc;
+            std::vector<float> hwr((size_t)cout * cinp, 0.f);
+            for (int co = 0; co < cout; ++co) {
+                for (int ci = 0; ci < cin; ++ci) hwr[(size_t)co * cinp + ci] = scr[co] * Wr->v[(size_t)co * cin + ci];
+                hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
+            }
+            if ((rc = wr.upload(hwr))) return rc;
+        }
+        std::vector<float> ha(A_eff.begin(), A_eff.end());
+        if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
+            (rc = biasT.upload(hbt)))
+            return rc;
+        return TIK_OK;
+    }
+
+    static int tout(int tin, int s) { return (tin - 1) / s + 1; }   // kt=3, pad=1
+
+    // x: rows (N*tin*V) of ld floats (>= cinp, %4); z: workspace N*tin*V*cout;
+    // out: rows (N*tout*V) of cout floats.
+    int forward(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st) const {
+        const int to = tout(tin, stride);
+        tik::CgemmArgs g{};
+        g.M = N * tin * V; g.Nc = cout; g.V = V; g.tout = tin;
+        g.seg[0] = tik::Seg{x, wg.p, cinp, ld, 1, 1, 0, tin, cinp};
+        g.nseg = 1;
+        g.bias = bias2.p; g.out = z; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
+        const double px_in = (double)N * tin * V, px_out = (double)N * to * V;
+        {
+            ProfScope p("G272x64.gcn_mix", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                        4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+            HIP_TRY(tik::launch_cgemm(g, tik::CFG_G272x64, st));
+        }
+
+        tik::CgemmArgs t{};
+        t.M = N * to * V; t.Nc = cout; t.V = V; t.tout = to;
+        t.seg[0] = tik::Seg{z, wt.p, cout, cout, TK, stride, 1, tin, TK * cout};
+        t.nseg = 1;
+        if (res == RES_CONV) {
+            t.seg[1] = tik::Seg{x, wr.p, cinp, ld, 1, stride, 0, tin, cinp};
+            t.nseg = 2;
+        } else if (res == RES_IDEN) {
+            t.resid = x; t.ldr = ld;
+        }
+        t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
+        const bool big = cout >= 128;
+        double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
+        if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
+        if (res == RES_IDEN) by += 4.0 * px_out * cout;
+        {
+            ProfScope p(big ? "T128x128.tcn_res" : "T128x64.tcn_res", fl, by, st);
+            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T128x64, st));
+        }
+        return TIK_OK;
+    }
+};
+
+}  // namespace
+
+// ----------------------------------------------------------------------------
+struct tik_model {
+    int V = 17, C0 = 3, feat = 0, hidden = 0, pose_dim = 0;
+    std::vector<Layer> layers;
+    DevBuf bn_sc, bn_sh;           // data_bn (V*C0)
+    DevBuf w0, b0, w3, b3;         // head
+    DevBuf xb, z, a0, a1, hid;     // workspace
+    Profiler prof;
+    bool profiling = false;
+};
+
+struct ProfGuard {
+    ProfGuard(tik_model* m) { g_prof = (m && m->profiling) ? &m->prof : nullptr; }
+    ~ProfGuard() { g_prof = nullptr; }
+};
+
+struct tik_block {
+    Layer layer;
+    DevBuf xp, z;   // padded-input and z workspace
+};
+
+extern "C" {
+
+const char* tik_last_error(void) { return g_err.c_str(); }
+const char* tik_version(void) { return "tik 0.1.0 (gfx950, fp32 MFMA)"; }
+
+int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out) {
+    if (!tensors || n_tensors <= 0 || !out) return fail(TIK_E_INVALID, "tik_model_create: null argument");
+    *out = nullptr;
+    TensorMap m = to_map(tensors, n_tensors);
+    const HostTensor* A = find(m, "backbone.A");
+    if (!A) return fail(TIK_E_MISSING, "missing 'backbone.A'");
+    if (A->shape.size() != 3 || A->shape[1] != A->shape[2])
+        return fail(TIK_E_INVALID, "'backbone.A' must be (K,V,V)");
+    if (A->shape[0] != 1) return fail(TIK_E_INVALID, "only the 'uniform' graph strategy (K=1) is supported by the fused path");
+    auto* md = new tik_model();
+    md->V = (int)A->shape[1];
+    if (md->V != 17) { delete md; return fail(TIK_E_INVALID, "fused path is built for V=17 (coco), got %d", (int)A->shape[1]); }
+    const int V = md->V;
+    int rc;
+    // data_bn
+    {
+        std::vector<float> sc, sh;
+        const HostTensor* g = find(m, "backbone.data_bn.weight");
+        if (!g) { delete md; return fail(TIK_E_MISSING, "missing 'backbone.data_bn.weight'"); }
+        md->C0 = (int)g->v.size() / V;
+        if (md->C0 * V != (int)g->v.size() || md->C0 > 4) { delete md; return fail(TIK_E_INVALID, "data_bn size %zu not V*C (C<=4)", g->v.size()); }
+        if ((rc = bn_fold(m, "backbone.data_bn", V * md->C0, sc, sh))) { delete md; return rc; }
+        if ((rc = md->bn_sc.upload(sc)) || (rc = md->bn_sh.upload(sh))) { delete md; return rc; }
+    }
+    int cin = md->C0;
+    for (int l = 0;; ++l) {
+        const std::string pre = "backbone.st_gcn_networks." + std::to_string(l) + ".";
+        const HostTensor* Wg = find(m, pre + "gcn.conv.weight");
+        if (!Wg) break;
+        const int cout = (int)Wg->shape[0];
+        if ((int)Wg->shape[1] != cin) { delete md; return fail(TIK_E_INVALID, "layer %d: in_channels %d != previous out %d", l, (int)Wg->shape[1], cin); }
+        // Temporal strides are architecture, not weights: the IK config of
+        // pose_trainer.py:76-83 unless the caller passes a "tik.strides" tensor.
+        static const int ik_strides[8] = {1, 1, 2, 1, 1, 2, 2, 2};
+        int stride = l < 8 ? ik_strides[l] : 1;
+        if (const HostTensor* s = find(m, "tik.strides")) {
+            if (l >= (int)s->v.size()) { delete md; return fail(TIK_E_INVALID, "'tik.strides' has no entry for layer %d", l); }
+            stride = (int)s->v[l];
+        }
+        const HostTensor* Wr = find(m, pre + "residual.0.weight");
+        if ((Wr != nullptr) != (cin != cout || stride != 1)) {
+            delete md;
+            return fail(TIK_E_INVALID, "layer %d: residual conv presence does not match (cin=%d, cout=%d, stride=%d)", l, cin, cout, stride);
+        }
+        const HostTensor* imp = find(m, "backbone.edge_importance." + std::to_string(l));
+        std::vector<float> Ae(V * V);
+        for (int i = 0; i < V * V; ++i) Ae[i] = A->v[i] * (imp ? imp->v[i] : 1.0f);
+        md->layers.emplace_back();
+        if ((rc = md->layers.back().build(m, pre, cin, cout, stride, 1, Ae, V))) { delete md; return rc; }
+        cin = cout;
+    }
+    if (md->layers.empty()) { delete md; return fail(TIK_E_MISSING, "no 'backbone.st_gcn_networks.*' layers"); }
+    const HostTensor* W0 = find(m, "pose_regressor.0.weight");
+    const HostTensor* B0 = find(m, "pose_regressor.0.bias");
+    const HostTensor* W3 = find(m, "pose_regressor.3.weight");
+    const HostTensor* B3 = find(m, "pose_regressor.3.bias");
+    if (!W0 || !B0 || !W3 || !B3) { delete md; return fail(TIK_E_MISSING, "missing pose_regressor.{0,3}.{weight,bias}"); }
+    md->feat = V * cin;
+    md->hidden = (int)W0->shape[0];
+    md->pose_dim = (int)W3->shape[0];
+    if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
+    if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
+    if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v))) {
+        delete md;
+        return rc;
+    }
+    *out = md;
+    return TIK_OK;
+}
+
+int tik_model_destroy(tik_model_t m) {
+    delete m;
+    return TIK_OK;
+}
+
+int tik_model_out_frames(tik_model_t m, int T) {
+    if (!m || T <= 0) return fail(TIK_E_INVALID, "bad model/T");
+    for (const Layer& L : m->layers) T = Layer::tout(T, L.stride);
+    return T;
+}
+
+int tik_model_reserve(tik_model_t m, int N, int T) {
+    if (!m || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_model_reserve: bad arguments");
+    const size_t V = m->V;
+    size_t zmax = 0, amax = 0;
+    int t = T;
+    for (const Layer& L : m->layers) {
+        zmax = std::max(zmax, (size_t)N * t * V * L.cout);
+        t = Layer::tout(t, L.stride);
+        amax = std::max(amax, (size_t)N * t * V * L.cout);
+    }
+    int rc;
+    if ((rc = m->xb.reserve((size_t)N * T * V * 4)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
+        (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
+        return rc;
+    return TIK_OK;
+}
+
+static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st) {
+    int rc;
+    if ((rc = tik_model_reserve(m, N, T))) return rc;
+    const int V = m->V;
+    {
+        const double px = (double)N * T * V;
+        ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
+        HIP_TRY(tik::launch_data_bn(x, N * T * V, V, m->C0, m->bn_sc.p, m->bn_sh.p, m->xb.p, st));
+    }
+    const float* cur = m->xb.p;
+    int ld = 4, t = T;
+    float* bufs[2] = {m->a0.p, m->a1.p};
+    int which = 0;
+    for (const Layer& L : m->layers) {
+        float* o = bufs[which];
+        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st))) return rc;
+        cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
+    }
+    *feat_out = const_cast<float*>(cur);
+    *tout = t;
+    return TIK_OK;
+}
+
+int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream) {
+    if (!m || !x || !feat || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_backbone_forward: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    ProfGuard pg(m);
+    float* f;
+    int to, rc;
+    if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
+    HIP_TRY(hipMemcpyAsync(feat, f, sizeof(float) * (size_t)N * to * m->feat, hipMemcpyDeviceToDevice, st));
+    return TIK_OK;
+}
+
+int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream) {
+    if (!m || !x || !poses || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    ProfGuard pg(m);
+    float* f;
+    int to, rc;
+    if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
+    const int rows = N * to;
+    tik::CgemmArgs h{};
+    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
+    h.seg[0] = tik::Seg{f, m->w0.p, m->feat, m->feat, 1, 1, 0, rows, m->feat};
+    h.nseg = 1; h.bias = m->b0.p; h.out = m->hid.p; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
+    {
+        ProfScope pr("H64x128.head0", 2.0 * rows * m->feat * m->hidden,
+                     4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
+        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x128, st));
+    }
+    tik::CgemmArgs p{};
+    p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
+    p.seg[0] = tik::Seg{m->hid.p, m->w3.p, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden};
+    p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
+    {
+        ProfScope pr("H64x128.head3", 2.0 * rows * m->hidden * m->pose_dim,
+                     4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
+        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x128, st));
+    }
+    return TIK_OK;
+}
+
+int tik_model_profile(tik_model_t m, int max_launches) {
+    if (!m || max_launches < 0) return fail(TIK_E_INVALID, "tik_model_profile: bad arguments");
+    m->profiling = max_launches > 0;
+    return max_launches > 0 ? m->prof.enable(max_launches) : (m->prof.clear(), TIK_OK);
+}
+
+int tik_model_profile_count(tik_model_t m) {
+    if (!m) return fail(TIK_E_INVALID, "null model");
+    return (int)m->prof.recs.size();
+}
+
+int tik_model_profile_read(tik_model_t m, int i, char* label, int label_len, float* ms, double* flops,
+                           double* bytes) {
+    if (!m || i < 0 || i >= (int)m->prof.recs.size()) return fail(TIK_E_INVALID, "tik_model_profile_read: bad index");
+    const auto& r = m->prof.recs[i];
+    if (label && label_len > 0) {
+        strncpy(label, r.label.c_str(), label_len - 1);
+        label[label_len - 1] = 0;
+    }
+    if (flops) *flops = r.flops;
+    if (bytes) *bytes = r.bytes;
+    if (ms) HIP_TRY(hipEventElapsedTime(ms, m->prof.ev0[i], m->prof.ev1[i]));
+    return TIK_OK;
+}
+
+// ---------------------------------------------------------------------------- block API
+int tik_block_create(const tik_tensor* tensors, int n_tensors, int in_channels, int out_channels, int stride,
+                     int residual, const float* A_eff_host, int V, tik_block_t* out) {
+    if (!tensors || !A_eff_host || !out || in_channels <= 0 || out_channels <= 0 || stride <= 0 || V <= 0)
+        return fail(TIK_E_INVALID, "tik_block_create: bad arguments");
+    if (V != 17) return fail(TIK_E_INVALID, "fused block kernel is built for V=17 (coco layout), got V=%d", V);
+    TensorMap m = to_map(tensors, n_tensors);
+    auto* b = new tik_block();
+    std::vector<float> Ae(A_eff_host, A_eff_host + V * V);
+    int rc = b->layer.build(m, "", in_channels, out_channels, stride, residual, Ae, V);
+    if (rc) { delete b; return rc; }
+    *out = b;
+    return TIK_OK;
+}
+
+int tik_block_destroy(tik_block_t b) {
+    delete b;
+    return TIK_OK;
+}
+
+int tik_stgcn_block_fwd(tik_block_t b, const float* x, int N, int T, float* out, void* stream) {
+    if (!b || !x || !out || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_stgcn_block_fwd: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    const Layer& L = b->layer;
+    const size_t rows = (size_t)N * T * L.V;
+    int rc;
+    const float* xin = x;
+    if (L.cin != L.cinp) {
+        if ((rc = b->xp.reserve(rows * L.cinp))) return rc;
+        HIP_TRY(tik::launch_pad_channels(x, (long long)rows, L.cin, L.cinp, b->xp.p, st));
+        xin = b->xp.p;
+    }
+    if ((rc = b->z.reserve(rows * L.cout))) return rc;
+    return L.forward(xin, L.cinp, N, T, b->z.p, out, st);
+}
+
+// ---------------------------------------------------------------------------- ops
+int tik_gconv_fwd(const float* x, int N, int Cin, int T, int V, const float* A, int K, const float* W,
+                  const float* b, int Cout, int t_kernel, int t_stride, int t_padding, int t_dilation, float* out,
+                  void* stream) {
+    if (!x || !A || !W || !out || N <= 0 || Cin <= 0 || T <= 0 || V <= 0 || K <= 0 || Cout <= 0 || t_kernel <= 0 ||
+        t_stride <= 0 || t_padding < 0 || t_dilation <= 0)
+        return fail(TIK_E_INVALID, "tik_gconv_fwd: bad arguments");
+    const int To = (T + 2 * t_padding - t_dilation * (t_kernel - 1) - 1) / t_stride + 1;
+    if (To <= 0) return fail(TIK_E_INVALID, "tik_gconv_fwd: empty temporal output");
+    if ((size_t)K * Cout * V * sizeof(float) > 160 * 1024)
+        return fail(TIK_E_INVALID, "tik_gconv_fwd: K*Cout*V=%d exceeds the per-frame LDS tile", K * Cout * V);
+    HIP_TRY(tik::launch_gconv(x, N, Cin, T, V, A, K, W, b, Cout, t_kernel, t_stride, t_padding, t_dilation, To, out,
+                              (hipStream_t)stream));
+    return TIK_OK;
+}
+
+int tik_aa_to_rotmat(const float* aa, int n, float* R, void* stream) {
+    if (!aa || !R || n < 0) return fail(TIK_E_INVALID, "tik_aa_to_rotmat: bad arguments");
+    HIP_TRY(tik::launch_aa_to_rotmat(aa, n, R, (hipStream_t)stream));
+    return TIK_OK;
+}
+
+int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h, int root_a, int root_b,
+                      int relative, float* windows, void* stream) {
+    if (!seq || !windows || F <= 0 || V <= 0 || n_idx < 0 || h < 0 || idx0 < 0 || idx0 + n_idx > F)
+        return fail(TIK_E_INVALID, "tik_window_gather: bad arguments");
+    if (relative && (root_a < 0 || root_a >= V || root_b < 0 || root_b >= V))
+        return fail(TIK_E_INVALID, "tik_window_gather: root joints out of range");
+    // data_amass.py:27-29 raises when h > idx > F - h; a window that overruns
+    // both ends of a short sequence comes back shorter than 2h+1 there.
+    for (int i = idx0; i < idx0 + n_idx; ++i) {
+        if (h > i && i > F - h)
+            return fail(TIK_E_INVALID, "h_win_size > idx > arr.shape[0] - h_win_size: %d > %d > %d - %d", h, i, F, h);
+        if (i - h < 0 && i + h > F - 1 && i <= F - h)
+            return fail(TIK_E_INVALID, "window at idx %d overruns both ends (reference returns a short window)", i);
+    }
+    HIP_TRY(tik::launch_window_gather(seq, F, V, idx0, n_idx, h, root_a, root_b, relative, windows,
+                                      (hipStream_t)stream));
+    return TIK_OK;
+}
+
+}  // extern "C"

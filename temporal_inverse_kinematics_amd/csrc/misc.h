@@ -1,0 +1,17 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tik {
+
+hipError_t launch_data_bn(const float* x, int n_px, int V, int C, const float* scale,
+                          const float* shift, float* xb, hipStream_t st);
+hipError_t launch_aa_to_rotmat(const float* aa, int n, float* R, hipStream_t st);
+hipError_t launch_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h, int ra,
+                                int rb, int relative, float* out, hipStream_t st);
+hipError_t launch_gconv(const float* x, int N, int Cin, int T, int V, const float* A, int K,
+                        const float* W, const float* b, int Cout, int tk, int ts, int tp, int td,
+                        int To, float* out, hipStream_t st);
+
+hipError_t launch_pad_channels(const float* x, long long rows, int C, int Cp, float* y, hipStream_t st);
+
+}  // namespace tik

@@ -1,0 +1,65 @@
+"""The N>1 path on CPU: world_size-2 gloo processes shard a global batch
+contiguously and all-gather the per-rank pose blocks in rank order (the
+compute is injected: the HIP forward has no CPU path)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from temporal_inverse_kinematics_amd.distributed import gather_poses, shard_range, sharded_forward
+    g = torch.arange(n * 4 * 66, dtype=torch.float32).reshape(n, 4, 66)
+    seen = []
+
+    def fwd(x):
+        seen.append(x.shape[0])
+        return x * 2 + 1
+
+    out = sharded_forward(fwd, g)
+    ok = torch.equal(out, g * 2 + 1)
+    lo, hi = shard_range(n, rank, world)
+    ok = ok and seen == [hi - lo]
+    if n % world == 0:
+        local = g[lo:hi] + rank
+        full = gather_poses(local)
+        exp = torch.cat([g[shard_range(n, r, world)[0]:shard_range(n, r, world)[1]] + r for r in range(world)])
+        ok = ok and torch.equal(full, exp)
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [8, 7])
+def test_sharded_gather_gloo_ws2(n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: True, 1: True}
+
+
+def test_shard_range_covers():
+    from temporal_inverse_kinematics_amd.distributed import shard_range
+    for n in [0, 1, 7, 8, 1023, 8192]:
+        for w in [1, 2, 3, 8]:
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))

@@ -1,0 +1,139 @@
+"""GPU parity of the HIP IK path (through libtik.so) against the golden fixtures
+made by the reference and against the CPU oracle. Tolerance: 1e-4 abs on the
+66-d poses (BASELINE.json north_star); features/blocks 1e-4 abs on O(1-5)
+activations (fp32 MFMA, BN folded)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import stgcn as orc
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def model():
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    return synthetic_model(win_size=64, device="cuda")
+
+
+@pytest.fixture(scope="module")
+def sd(model):
+    return {k: v.detach().cpu().numpy() for k, v in model.regressor.state_dict().items()}
+
+
+@pytest.mark.parametrize("T", [64, 65, 9, 17])
+def test_model_vs_golden(model, T):
+    m = golden("model.npz")
+    x = torch.from_numpy(m[f"T{T}|x"]).cuda()
+    with torch.no_grad():
+        y = model(x)["poses"].cpu().numpy()
+        f = model.regressor.backbone_features(x).cpu().numpy()
+    assert y.shape == m[f"T{T}|y"].shape
+    assert np.abs(f - m[f"T{T}|feat"]).max() < TOL
+    assert np.abs(y - m[f"T{T}|y"]).max() < TOL
+
+
+@pytest.mark.parametrize("N,T", [(1, 1), (1, 2), (3, 3), (2, 5), (5, 31), (2, 100), (37, 64)])
+def test_model_ragged_vs_oracle(model, sd, N, T):
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    x = syn.synthetic_windows(N, T, seed=1000 + T)
+    with torch.no_grad():
+        y = model(torch.from_numpy(x).cuda())["poses"].cpu().numpy()
+    ref = orc.pose_regressor(x, sd)["poses"]
+    assert y.shape == ref.shape
+    assert np.abs(y - ref).max() < TOL
+
+
+def test_model_full_batch_consistency(model, sd):
+    """Config #2 size (1024 x 64): every window equals its solo solve (batch
+    independence), sampled windows match the oracle, and a checksum of the
+    per-window sums is deterministic across two launches."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    x = syn.synthetic_windows(1024, 64, seed=0)
+    xd = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        y1 = model(xd)["poses"]
+        y2 = model(xd)["poses"]
+        solo = torch.cat([model(xd[i:i + 1])["poses"] for i in (0, 511, 1023)])
+    assert torch.equal(y1, y2)
+    assert (y1[[0, 511, 1023]] - solo).abs().max().item() == 0.0
+    pick = [0, 1, 255, 700, 1023]
+    ref = orc.pose_regressor(x[pick], sd)["poses"]
+    assert np.abs(y1.cpu().numpy()[pick] - ref).max() < TOL
+    assert torch.isfinite(y1).all()
+
+
+def test_run_inference_sample(model):
+    from temporal_inverse_kinematics_amd.inference import run_inference, synthetic_model
+    r = golden("run_inference.npz")
+    y64 = run_inference(model, r["seq"])
+    assert y64.dtype == np.float32 and y64.shape == (231, 66)
+    assert np.abs(y64 - r["win64"]).max() < TOL
+    m9 = synthetic_model(win_size=9, device="cuda")
+    y9 = run_inference(m9, r["seq"])
+    assert np.abs(y9 - r["win9"]).max() < TOL
+
+
+def test_blocks_vs_golden():
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.models import StGcnBlock
+    b = golden("blocks.npz")
+    for tag in ["conv_l0", "iden_l1", "conv_s2_l2", "zero"]:
+        cin, cout, s, residual = [int(v) for v in b[f"{tag}|cfg"]]
+        blk = StGcnBlock(cin, cout, (3, 1), stride=s, residual=bool(residual))
+        sdb = syn.block_state_dict("", cin, cout, s, residual=bool(residual), seed=5)
+        blk.load_state_dict({k: torch.from_numpy(v) for k, v in sdb.items()}, strict=False)
+        blk = blk.cuda().eval()
+        A = torch.from_numpy(b["A"] * b[f"{tag}|imp"]).cuda()
+        for T in [9, 16]:
+            with torch.no_grad():
+                y, _ = blk(torch.from_numpy(b[f"{tag}|T{T}|x"]).cuda(), A)
+            assert np.abs(y.cpu().numpy() - b[f"{tag}|T{T}|y"]).max() < TOL, (tag, T)
+
+
+def test_gconv_vs_golden():
+    from temporal_inverse_kinematics_amd.st_gcn import ConvTemporalGraphical
+    g = golden("gconv.npz")
+    A = torch.from_numpy(g["A"]).cuda()
+    for tag in ["k5_t1", "k5_t3", "k5_t3d2"]:
+        cin, cout, tk, ts, tp, td, bias = [int(v) for v in g[f"{tag}|cfg"]]
+        op = ConvTemporalGraphical(cin, cout, A.shape[0], tk, ts, tp, td, bool(bias))
+        st = {"conv.weight": torch.from_numpy(g[f"{tag}|conv.weight"])}
+        if bias:
+            st["conv.bias"] = torch.from_numpy(g[f"{tag}|conv.bias"])
+        op.load_state_dict(st)
+        op = op.cuda()
+        with torch.no_grad():
+            y, _ = op(torch.from_numpy(g[f"{tag}|x"]).cuda(), A)
+        assert np.abs(y.cpu().numpy() - g[f"{tag}|y"]).max() < 1e-5, tag
+
+
+def test_aa_to_rotmat_vs_kornia():
+    from temporal_inverse_kinematics_amd.rotation import angle_axis_to_rotation_matrix
+    k = golden("kornia.npz")
+    R = angle_axis_to_rotation_matrix(torch.from_numpy(k["aa"]).cuda()).cpu().numpy()
+    assert np.abs(R - k["R"]).max() < 2e-6
+
+
+def test_window_gather_vs_reference():
+    from temporal_inverse_kinematics_amd.windowing import gather_windows
+    w = golden("windowing.npz")
+    seq = torch.from_numpy(w["ids_in"]).cuda()
+    got = gather_windows(seq, 9).cpu().numpy()
+    assert np.abs(got - w["ids_items"]).max() < 1e-6
+    arr20 = torch.from_numpy(w["arr20"]).cuda()
+    with pytest.raises(ValueError):
+        gather_windows(arr20, 64, idx0=5, n=1)
+    got = gather_windows(arr20, 16, relative_pose=False).cpu().numpy()
+    for idx in [0, 1, 10, 18, 19]:
+        assert np.array_equal(got[idx], w[f"sw|20|{idx}|8"])
+
+
+def test_cpu_tensor_refused(model):
+    with pytest.raises(RuntimeError):
+        model(torch.zeros(1, 9, 17, 3))

@@ -73,9 +73,20 @@ const HostTensor* find(const TensorMap& m, const std::string& k) {
     return it == m.end() ? nullptr : &it->second;
 }
 
-struct DevBuf {
+struct DevBuf {   // owning device buffer; move-only (a copy would double-free)
     float* p = nullptr;
     size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            if (p) (void)hipFree(p);
+            p = o.p; n = o.n; o.p = nullptr; o.n = 0;
+        }
+        return *this;
+    }
     ~DevBuf() { if (p) (void)hipFree(p); }
     int upload(const std::vector<float>& h) {
         if (p) { (void)hipFree(p); p = nullptr; }

@@ -216,6 +216,7 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     const dim3 blk(256);
+    (void)hipGetLastError();   // drop a stale error left by earlier runtime calls (not ours)
     switch (cfg) {
         case CFG_T128x128: {
             dim3 g((a.M + 127) / 128, (a.Nc + 127) / 128);

@@ -27,6 +27,7 @@ __global__ void data_bn_kernel(const float* __restrict__ x, int n_px, int V, int
 hipError_t launch_data_bn(const float* x, int n_px, int V, int C, const float* scale,
                           const float* shift, float* xb, hipStream_t st) {
     if (n_px <= 0) return hipSuccess;
+    (void)hipGetLastError();  // drop a stale error left by earlier runtime calls
     hipLaunchKernelGGL(data_bn_kernel, dim3((n_px + 255) / 256), dim3(256), 0, st, x, n_px, V, C,
                        scale, shift, xb);
     return hipGetLastError();
@@ -61,6 +62,7 @@ __global__ void aa_to_rotmat_kernel(const float* __restrict__ aa, int n, float* 
 
 hipError_t launch_aa_to_rotmat(const float* aa, int n, float* R, hipStream_t st) {
     if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();  // drop a stale error left by earlier runtime calls
     hipLaunchKernelGGL(aa_to_rotmat_kernel, dim3((n + 255) / 256), dim3(256), 0, st, aa, n, R);
     return hipGetLastError();
 }
@@ -95,6 +97,7 @@ hipError_t launch_window_gather(const float* seq, int F, int V, int idx0, int n_
                                 int rb, int relative, float* out, hipStream_t st) {
     const long long total = (long long)n_idx * (2 * h + 1) * V;
     if (total <= 0) return hipSuccess;
+    (void)hipGetLastError();  // drop a stale error left by earlier runtime calls
     hipLaunchKernelGGL(window_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        seq, F, V, idx0, n_idx, h, ra, rb, relative, out);
     return hipGetLastError();
@@ -144,6 +147,7 @@ hipError_t launch_gconv(const float* x, int N, int Cin, int T, int V, const floa
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         if (e != hipSuccess) return e;
     }
+    (void)hipGetLastError();  // drop a stale error left by earlier runtime calls
     hipLaunchKernelGGL(gconv_kernel, dim3(To, N), dim3(256), shm, st, x, Cin, T, V, A, K, W, b, Cout,
                        tk, ts, tp, td, To, out);
     return hipGetLastError();
@@ -162,6 +166,7 @@ __global__ void pad_channels_kernel(const float* __restrict__ x, long long rows,
 hipError_t launch_pad_channels(const float* x, long long rows, int C, int Cp, float* y, hipStream_t st) {
     const long long total = rows * Cp;
     if (total <= 0) return hipSuccess;
+    (void)hipGetLastError();  // drop a stale error left by earlier runtime calls
     hipLaunchKernelGGL(pad_channels_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x,
                        rows, C, Cp, y);
     return hipGetLastError();

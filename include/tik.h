@@ -113,6 +113,31 @@ int tik_aa_to_rotmat(const float* aa, int n, float* R, void* stream);
 int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h, int root_a,
                       int root_b, int relative, float* windows, void* stream);
 
+/* ------------------------------------------------------------------------
+ * SMPL-X forward kinematics + linear blend skinning (the FK check).
+ * Replaces common/smpl_util.py:8-82 (load_smplx_models / run_smpl_inference)
+ * and the third-party smplx.SMPLX.forward it calls (smpl_util.py:67-69;
+ * create(model_type='smplx', use_pca=False, use_face_contour=True)).
+ *
+ * tik_fk_create: named host tensors (integer tables passed as exact floats):
+ *   v_template (V,3), shapedirs (V,3,nb), [exprdirs (V,3,ne)], posedirs (486,3V),
+ *   J_regressor (55,V), lbs_weights (V,55), parents (55), faces (F,3),
+ *   lmk_faces_idx (L), lmk_bary_coords (L,3), extra_verts (21),
+ *   [pose_mean (55,3)] (flat_hand_mean=False hand mean),
+ *   [dynamic_lmk_faces_idx (79,D), dynamic_lmk_bary_coords (79,D,3)].
+ * flags bit 0: use_face_contour (needs the dynamic tables).
+ * tik_fk_forward: full_pose (B,55,3) [global, 21 body, jaw, leye, reye,
+ *   15 lhand, 15 rhand], betas (B,nb)/NULL, expression (B,ne)/NULL,
+ *   transl (B,3)/NULL -> joints (B, 55+21+L+D, 3), verts (B,V,3) or NULL.
+ * ---------------------------------------------------------------------- */
+int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t* out);
+int tik_fk_destroy(tik_fk_t fk);
+int tik_fk_num_joints(tik_fk_t fk);
+int tik_fk_num_verts(tik_fk_t fk);
+int tik_fk_reserve(tik_fk_t fk, int B);
+int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, const float* expression,
+                   const float* transl, int B, float* joints, float* verts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

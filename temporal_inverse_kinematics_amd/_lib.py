@@ -48,6 +48,12 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_gconv_fwd": (_I, (_P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P)),
     "tik_aa_to_rotmat": (_I, (_P, _I, _P, _P)),
     "tik_window_gather": (_I, (_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P)),
+    "tik_fk_create": (_I, (ctypes.POINTER(TikTensor), _I, _I, ctypes.POINTER(_P))),
+    "tik_fk_destroy": (_I, (_P,)),
+    "tik_fk_num_joints": (_I, (_P,)),
+    "tik_fk_num_verts": (_I, (_P,)),
+    "tik_fk_reserve": (_I, (_P, _I)),
+    "tik_fk_forward": (_I, (_P, _P, _P, _P, _P, _I, _P, _P, _P)),
 }
 
 _lib = None

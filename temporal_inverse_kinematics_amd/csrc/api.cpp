@@ -21,90 +21,14 @@
 #include "../../include/tik.h"
 #include "cgemm.h"
 #include "misc.h"
+#include "common.h"
+
+namespace tik_host {
+thread_local std::string g_err;
+}
+using namespace tik_host;
 
 namespace {
-
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) {
-    char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-#define HIP_TRY(expr)                                                                        \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess) return fail(TIK_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-    } while (0)
-
-constexpr float BN_EPS = 1e-5f;
-constexpr int TK = 3;   // temporal kernel (pose_trainer.py:85)
-
-struct HostTensor {
-    std::vector<float> v;
-    std::vector<int64_t> shape;
-};
-
-using TensorMap = std::map<std::string, HostTensor>;
-
-TensorMap to_map(const tik_tensor* t, int n) {
-    TensorMap m;
-    for (int i = 0; i < n; ++i) {
-        if (!t[i].name) continue;
-        HostTensor h;
-        int64_t numel = 1;
-        for (int d = 0; d < t[i].ndim; ++d) {
-            h.shape.push_back(t[i].shape[d]);
-            numel *= t[i].shape[d];
-        }
-        if (t[i].data) h.v.assign(t[i].data, t[i].data + numel);
-        m[t[i].name] = std::move(h);
-    }
-    return m;
-}
-
-const HostTensor* find(const TensorMap& m, const std::string& k) {
-    auto it = m.find(k);
-    return it == m.end() ? nullptr : &it->second;
-}
-
-struct DevBuf {   // owning device buffer; move-only (a copy would double-free)
-    float* p = nullptr;
-    size_t n = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-    DevBuf& operator=(DevBuf&& o) noexcept {
-        if (this != &o) {
-            if (p) (void)hipFree(p);
-            p = o.p; n = o.n; o.p = nullptr; o.n = 0;
-        }
-        return *this;
-    }
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    int upload(const std::vector<float>& h) {
-        if (p) { (void)hipFree(p); p = nullptr; }
-        n = h.size();
-        if (n == 0) return TIK_OK;
-        if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) return fail(TIK_E_NOMEM, "hipMalloc(%zu floats) failed", n);
-        if (hipMemcpy(p, h.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
-            return fail(TIK_E_HIP, "hipMemcpy H2D failed");
-        return TIK_OK;
-    }
-    int reserve(size_t want) {
-        if (want <= n) return TIK_OK;
-        if (p) { (void)hipFree(p); p = nullptr; }
-        if (hipMalloc(&p, want * sizeof(float)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu floats) failed", want); }
-        n = want;
-        return TIK_OK;
-    }
-};
 
 int round4(int c) { return (c + 3) & ~3; }
 

@@ -12,14 +12,16 @@
 //   * head Linear layers    pose_trainer.py:89-92        (V=1, tout=M)
 // Epilogues: bias (+ identity residual) + {none, ReLU, LeakyReLU}; or the
 // graph epilogue: per-frame V-mix  z[w] = sum_v A[v][w] y[v]  (the einsum of
-// gconv_origin.py:64) + folded BN bias + ReLU (st_gcn_aaai18.py:178-179).
+// gconv_origin.py:64) + folded BN bias + ReLU (st_gcn_aaai18.py:178-179);
+// or the skinning epilogue of SMPL-X LBS (rows = body*16 + transform entry,
+// cols = vertices): verts[b][v] = T_v(b)[:3,:3] v_posed[b][v] + T_v(b)[:3,3] (+ transl).
 #pragma once
 #include <hip/hip_runtime.h>
 
 namespace tik {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
-enum { EPI_BIAS = 0, EPI_GRAPH = 1 };
+enum { EPI_BIAS = 0, EPI_GRAPH = 1, EPI_SKIN = 2 };
 
 struct Seg {
     const float* src;   // rows of `ld` floats, cin used (cin % 4 == 0)
@@ -38,6 +40,7 @@ struct CgemmArgs {
     int ldo;
     const float* amix;   // EPI_GRAPH: [V][V], A_eff[v][w]
     int act;
+    // EPI_SKIN: resid = v_posed [B][ldr], out = verts [B][ldo], bias = transl [B][3] or null
 };
 
 // Tile configurations.
@@ -46,6 +49,7 @@ enum CgemmCfg {
     CFG_T128x64 = 1,    // BM=128, BN=64,  waves 2x2 : tcn of 64-channel layers
     CFG_G272x64 = 2,    // BM=272 (16 frames x 17 joints), BN=64, waves 1x4 : gcn + V-mix
     CFG_H64x128 = 3,    // BM=64,  BN=128, waves 2x2 : head Linear layers
+    CFG_S128x128 = 4,   // BM=128 (8 bodies x 16), BN=128 vertices, waves 2x2 : LBS skinning
 };
 
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st);

@@ -176,6 +176,28 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
                     a.out[(size_t)row * a.ldo + col] = v;
                 }
         }
+    } else if constexpr (EPI == EPI_SKIN) {
+        // rows r = b*16 + e, e = 4*row + col of the 3x4 transform T_v(b); lane
+        // group g = lane>>4 holds e = 4g..4g+3, i.e. transform row g (g < 3).
+        const int g = lane >> 4;
+        if (g < 3) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int b = (r0 + wm * FM * 16 + i * 16) >> 4;
+                if (b * 16 >= a.M) continue;
+                const float tb = a.bias ? a.bias[b * 3 + g] : 0.f;
+                const float* vp = a.resid + (size_t)b * a.ldr;
+                float* vo = a.out + (size_t)b * a.ldo;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int v = n0 + ccol0 + j * 16;
+                    if (v >= a.Nc) continue;
+                    const f32x4 t = acc[i][j];
+                    const float x = fmaf(t[0], vp[3 * v], fmaf(t[1], vp[3 * v + 1], fmaf(t[2], vp[3 * v + 2], t[3])));
+                    vo[3 * v + g] = x + tb;
+                }
+            }
+        }
     } else {
         // graph epilogue: BM = F frames * V joints, frame-aligned tiles.
         float* Cs = smem;
@@ -232,6 +254,11 @@ hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st) {
             if (a.V != 17) return hipErrorInvalidValue;
             dim3 g((a.M + 271) / 272, (a.Nc + 63) / 64);
             hipLaunchKernelGGL((cgemm_kernel<272, 64, 1, 4, EPI_GRAPH, 17>), g, blk, 0, st, a);
+            break;
+        }
+        case CFG_S128x128: {
+            dim3 g((a.M + 127) / 128, (a.Nc + 127) / 128);
+            hipLaunchKernelGGL((cgemm_kernel<128, 128, 2, 2, EPI_SKIN, 0>), g, blk, 0, st, a);
             break;
         }
         case CFG_H64x128: {

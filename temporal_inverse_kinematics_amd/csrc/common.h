@@ -1,0 +1,105 @@
+// common.h — host-side helpers shared by the C-ABI translation units:
+// thread-local last error, HIP error mapping, owning device buffers and the
+// state-dict view of a tik_tensor array.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/tik.h"
+
+namespace tik_host {
+
+extern thread_local std::string g_err;
+
+inline int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(TIK_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr float BN_EPS = 1e-5f;
+constexpr int TK = 3;   // temporal kernel (pose_trainer.py:85)
+
+struct HostTensor {
+    std::vector<float> v;
+    std::vector<int64_t> shape;
+};
+
+using TensorMap = std::map<std::string, HostTensor>;
+
+inline TensorMap to_map(const tik_tensor* t, int n) {
+    TensorMap m;
+    for (int i = 0; i < n; ++i) {
+        if (!t[i].name) continue;
+        HostTensor h;
+        int64_t numel = 1;
+        for (int d = 0; d < t[i].ndim; ++d) {
+            h.shape.push_back(t[i].shape[d]);
+            numel *= t[i].shape[d];
+        }
+        if (t[i].data) h.v.assign(t[i].data, t[i].data + numel);
+        m[t[i].name] = std::move(h);
+    }
+    return m;
+}
+
+inline const HostTensor* find(const TensorMap& m, const std::string& k) {
+    auto it = m.find(k);
+    return it == m.end() ? nullptr : &it->second;
+}
+
+template <class T>
+struct DevArray {   // owning device buffer; move-only (a copy would double-free)
+    T* p = nullptr;
+    size_t n = 0;
+    DevArray() = default;
+    DevArray(const DevArray&) = delete;
+    DevArray& operator=(const DevArray&) = delete;
+    DevArray(DevArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevArray& operator=(DevArray&& o) noexcept {
+        if (this != &o) {
+            if (p) (void)hipFree(p);
+            p = o.p; n = o.n; o.p = nullptr; o.n = 0;
+        }
+        return *this;
+    }
+    ~DevArray() { if (p) (void)hipFree(p); }
+    int upload(const std::vector<T>& h) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = h.size();
+        if (n == 0) return TIK_OK;
+        if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", h.size()); }
+        if (hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(TIK_E_HIP, "hipMemcpy H2D failed");
+        return TIK_OK;
+    }
+    int reserve(size_t want) {
+        if (want <= n) return TIK_OK;
+        if (p) { (void)hipFree(p); p = nullptr; }
+        if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", want); }
+        n = want;
+        return TIK_OK;
+    }
+};
+using DevBuf = DevArray<float>;
+using DevIBuf = DevArray<int>;
+
+
+}  // namespace tik_host

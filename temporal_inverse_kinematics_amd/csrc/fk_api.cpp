@@ -1,0 +1,233 @@
+// fk_api.cpp — C ABI of the SMPL-X FK check (include/tik.h, tik_fk_*).
+// Replaces common/smpl_util.py:8-82 (load_smplx_models / run_smpl_inference)
+// and the third-party smplx.SMPLX.forward it calls (lbs + landmarks).
+//
+// Per call (B bodies):
+//   fk_chain            R_j, J, A_j (B,16,64), pose feature (B,512), first 55 joints
+//   cgemm (T128x128)    v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
+//   cgemm (S128x128)    T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
+//   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cgemm.h"
+#include "common.h"
+#include "fk.h"
+
+using namespace tik_host;
+
+namespace {
+constexpr int NJ = 55;
+constexpr int KP = 512;   // padded blend-shape K (486 pose + 20 shape + 1 template)
+constexpr int KJ = 64;    // padded skinning K (55 joints)
+}  // namespace
+
+struct tik_fk {
+    int V = 0, F = 0, nb = 0, ne = 0, nlmk = 0, ndyn = 0, nextra = 0, njoints = 0;
+    bool contour = false;
+    DevBuf PT;         // [3V][KP]
+    DevBuf WT;         // [V][KJ]
+    DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
+    DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra;
+    int nchain = 0;
+    // workspace
+    DevBuf feat, ablk, vposed, verts_ws;
+    DevIBuf dyn_bin;
+    int cap = 0;
+};
+
+static const HostTensor* need(const TensorMap& m, const char* k, int& rc) {
+    const HostTensor* t = find(m, k);
+    if (!t) rc = fail(TIK_E_MISSING, "missing SMPL-X tensor '%s'", k);
+    return t;
+}
+
+static std::vector<int> to_int(const HostTensor* t) {
+    std::vector<int> o(t->v.size());
+    for (size_t i = 0; i < o.size(); ++i) o[i] = (int)std::lround(t->v[i]);
+    return o;
+}
+
+extern "C" {
+
+int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t* out) {
+    if (!tensors || n_tensors <= 0 || !out) return fail(TIK_E_INVALID, "tik_fk_create: null argument");
+    *out = nullptr;
+    TensorMap m = to_map(tensors, n_tensors);
+    int rc = TIK_OK;
+    const HostTensor* vt = need(m, "v_template", rc);
+    const HostTensor* sd = need(m, "shapedirs", rc);
+    const HostTensor* pd = need(m, "posedirs", rc);
+    const HostTensor* jr = need(m, "J_regressor", rc);
+    const HostTensor* lw = need(m, "lbs_weights", rc);
+    const HostTensor* par = need(m, "parents", rc);
+    const HostTensor* fc = need(m, "faces", rc);
+    const HostTensor* lf = need(m, "lmk_faces_idx", rc);
+    const HostTensor* lb = need(m, "lmk_bary_coords", rc);
+    const HostTensor* ex = need(m, "extra_verts", rc);
+    if (rc) return rc;
+    const HostTensor* ed = find(m, "exprdirs");
+    const HostTensor* pm = find(m, "pose_mean");
+    const HostTensor* df = find(m, "dynamic_lmk_faces_idx");
+    const HostTensor* db = find(m, "dynamic_lmk_bary_coords");
+    auto* fk = new tik_fk();
+    auto bad = [&](const char* msg) { delete fk; return fail(TIK_E_INVALID, "tik_fk_create: %s", msg); };
+    if (vt->shape.size() != 2 || vt->shape[1] != 3) return bad("v_template must be (V,3)");
+    const int V = fk->V = (int)vt->shape[0];
+    if (sd->shape.size() != 3 || sd->shape[0] != V || sd->shape[1] != 3) return bad("shapedirs must be (V,3,nb)");
+    fk->nb = (int)sd->shape[2];
+    fk->ne = ed ? (int)ed->shape[2] : 0;
+    if (ed && (ed->shape.size() != 3 || ed->shape[0] != V || ed->shape[1] != 3)) return bad("exprdirs must be (V,3,ne)");
+    const int NS = fk->nb + fk->ne;
+    if (54 * 9 + NS + 1 > KP || NS > 32) return bad("too many shape components");
+    if (pd->shape.size() != 2 || pd->shape[0] != 54 * 9 || pd->shape[1] != 3 * V) return bad("posedirs must be (486, 3V)");
+    if (jr->shape.size() != 2 || jr->shape[0] != NJ || jr->shape[1] != V) return bad("J_regressor must be (55,V)");
+    if (lw->shape.size() != 2 || lw->shape[0] != V || lw->shape[1] != NJ) return bad("lbs_weights must be (V,55)");
+    if ((int)par->v.size() != NJ) return bad("parents must have 55 entries");
+    if (fc->shape.size() != 2 || fc->shape[1] != 3) return bad("faces must be (F,3)");
+    fk->F = (int)fc->shape[0];
+    fk->nlmk = (int)lf->v.size();
+    fk->nextra = (int)ex->v.size();
+    if ((int)lb->v.size() != 3 * fk->nlmk) return bad("lmk_bary_coords must be (L,3)");
+    fk->contour = (flags & 1) && df && db;
+    fk->ndyn = fk->contour ? (int)df->shape[1] : 0;
+    if (fk->contour && (df->shape.size() != 2 || df->shape[0] != 79 || (int)db->v.size() != 79 * fk->ndyn * 3))
+        return bad("dynamic_lmk_faces_idx must be (79,D), dynamic_lmk_bary_coords (79,D,3)");
+    fk->njoints = NJ + fk->nextra + fk->nlmk + fk->ndyn;
+
+    // index validation (host side, once)
+    std::vector<int> hpar = to_int(par), hfaces = to_int(fc), hlf = to_int(lf), hex = to_int(ex);
+    for (int j = 0; j < NJ; ++j)
+        if (hpar[j] >= j || (j > 0 && hpar[j] < 0) || (j == 0 && hpar[j] != -1)) return bad("parents must be a topologically ordered tree rooted at 0");
+    for (int f : hfaces) if (f < 0 || f >= V) return bad("face vertex index out of range");
+    for (int f : hlf) if (f < 0 || f >= fk->F) return bad("landmark face index out of range");
+    for (int v : hex) if (v < 0 || v >= V) return bad("extra vertex index out of range");
+    std::vector<int> hdf;
+    if (fk->contour) {
+        hdf = to_int(df);
+        for (int f : hdf) if (f < 0 || f >= fk->F) return bad("dynamic landmark face index out of range");
+    }
+    // neck kinematic chain (smplx: from NECK_IDX=12 up to the root)
+    std::vector<int> chain;
+    for (int i = 12; i != -1; i = hpar[i]) chain.push_back(i);
+    fk->nchain = (int)chain.size();
+
+    // blend-shape matrix P^T (3V, KP): row 3v+c = [posedirs[:,3v+c] | shapedirs[v,c,:] | exprdirs[v,c,:] | v_template[v,c] | 0]
+    std::vector<float> PT((size_t)3 * V * KP, 0.f);
+    for (int v = 0; v < V; ++v)
+        for (int c = 0; c < 3; ++c) {
+            float* row = &PT[(size_t)(3 * v + c) * KP];
+            for (int p = 0; p < 486; ++p) row[p] = pd->v[(size_t)p * 3 * V + 3 * v + c];
+            for (int l = 0; l < fk->nb; ++l) row[486 + l] = sd->v[((size_t)v * 3 + c) * fk->nb + l];
+            for (int l = 0; l < fk->ne; ++l) row[486 + fk->nb + l] = ed->v[((size_t)v * 3 + c) * fk->ne + l];
+            row[486 + NS] = vt->v[(size_t)v * 3 + c];
+        }
+    std::vector<float> WT((size_t)V * KJ, 0.f);
+    for (int v = 0; v < V; ++v)
+        for (int j = 0; j < NJ; ++j) WT[(size_t)v * KJ + j] = lw->v[(size_t)v * NJ + j];
+    // J_regressor folded into the template and blend shapes (float64 on the host)
+    std::vector<float> jt(NJ * 3), jd((size_t)NJ * 3 * NS);
+    for (int j = 0; j < NJ; ++j)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0.0;
+            std::vector<double> d(NS, 0.0);
+            for (int v = 0; v < V; ++v) {
+                const double w = jr->v[(size_t)j * V + v];
+                if (w == 0.0) continue;
+                s += w * vt->v[(size_t)v * 3 + c];
+                for (int l = 0; l < fk->nb; ++l) d[l] += w * sd->v[((size_t)v * 3 + c) * fk->nb + l];
+                for (int l = 0; l < fk->ne; ++l) d[fk->nb + l] += w * ed->v[((size_t)v * 3 + c) * fk->ne + l];
+            }
+            jt[j * 3 + c] = (float)s;
+            for (int l = 0; l < NS; ++l) jd[((size_t)j * 3 + c) * NS + l] = (float)d[l];
+        }
+    std::vector<float> hpm(NJ * 3, 0.f);
+    if (pm) {
+        if ((int)pm->v.size() != NJ * 3) return bad("pose_mean must be (55,3)");
+        hpm = pm->v;
+    }
+    if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
+        (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
+        (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||
+        (rc = fk->extra.upload(hex))) {
+        delete fk;
+        return rc;
+    }
+    if (fk->contour && ((rc = fk->dyn_faces.upload(hdf)) || (rc = fk->dyn_bary.upload(db->v)))) {
+        delete fk;
+        return rc;
+    }
+    *out = fk;
+    return TIK_OK;
+}
+
+int tik_fk_destroy(tik_fk_t fk) {
+    delete fk;
+    return TIK_OK;
+}
+
+int tik_fk_num_joints(tik_fk_t fk) {
+    if (!fk) return fail(TIK_E_INVALID, "null fk handle");
+    return fk->njoints;
+}
+
+int tik_fk_num_verts(tik_fk_t fk) {
+    if (!fk) return fail(TIK_E_INVALID, "null fk handle");
+    return fk->V;
+}
+
+int tik_fk_reserve(tik_fk_t fk, int B) {
+    if (!fk || B <= 0) return fail(TIK_E_INVALID, "tik_fk_reserve: bad arguments");
+    if (B <= fk->cap) return TIK_OK;
+    int rc;
+    if ((rc = fk->feat.reserve((size_t)B * KP)) || (rc = fk->ablk.reserve((size_t)B * 16 * KJ)) ||
+        (rc = fk->vposed.reserve((size_t)B * 3 * fk->V)) || (rc = fk->dyn_bin.reserve((size_t)B)))
+        return rc;
+    fk->cap = B;
+    return TIK_OK;
+}
+
+int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, const float* expression,
+                   const float* transl, int B, float* joints, float* verts, void* stream) {
+    if (!fk || !full_pose || !joints || B <= 0) return fail(TIK_E_INVALID, "tik_fk_forward: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    int rc;
+    if ((rc = tik_fk_reserve(fk, B))) return rc;
+    float* vout = verts;
+    if (!vout) {
+        if ((rc = fk->verts_ws.reserve((size_t)B * 3 * fk->V))) return rc;
+        vout = fk->verts_ws.p;
+    }
+    tik::FkChainArgs c{};
+    c.B = B; c.nb = fk->nb; c.ne = fk->ne; c.kp = KP; c.kj = KJ; c.njoints = fk->njoints; c.nchain = fk->nchain;
+    c.pose = full_pose; c.betas = betas; c.expr = expression; c.transl = transl; c.pose_mean = fk->pose_mean.p;
+    c.parents = fk->parents.p; c.chain = fk->chain.p; c.jt = fk->jt.p; c.jd = fk->jd.p;
+    c.feat = fk->feat.p; c.ablk = fk->ablk.p; c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
+    HIP_TRY(tik::launch_fk_chain(c, st));
+
+    const int V3 = 3 * fk->V;
+    tik::CgemmArgs g{};   // v_posed = feat . P
+    g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
+    g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
+    g.nseg = 1; g.out = fk->vposed.p; g.ldo = V3; g.act = tik::ACT_NONE;
+    HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st));
+
+    tik::CgemmArgs s{};   // skinning + vertex transform
+    s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
+    s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
+    s.nseg = 1; s.resid = fk->vposed.p; s.ldr = V3; s.out = vout; s.ldo = V3; s.bias = transl;
+    HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st));
+
+    tik::FkLmkArgs l{};
+    l.B = B; l.V = fk->V; l.njoints = fk->njoints; l.nextra = fk->nextra; l.nlmk = fk->nlmk; l.ndyn = fk->ndyn;
+    l.verts = vout; l.transl = transl; l.extra = fk->extra.p; l.faces = fk->faces.p; l.lmk_faces = fk->lmk_faces.p;
+    l.lmk_bary = fk->lmk_bary.p; l.dyn_faces = fk->dyn_faces.p; l.dyn_bary = fk->dyn_bary.p;
+    l.dyn_bin = fk->dyn_bin.p; l.joints = joints;
+    HIP_TRY(tik::launch_fk_landmarks(l, st));
+    return TIK_OK;
+}
+
+}  // extern "C"

@@ -226,7 +226,9 @@ def synthetic_smplx_constants(seed: int = 1, num_verts: int = SMPLX_NUM_VERTS,
     (V,3,10), exprdirs (V,3,10), posedirs (486, V*3) [smplx stores it
     transposed to (P, V*3) at load time], J_regressor (55,V) non-negative with
     rows summing to 1, lbs_weights (V,55) softmax rows with <=4 dominant joints,
-    faces (F,3), landmark faces/barycentrics for the 51 static face landmarks.
+    faces (F,3), landmark faces/barycentrics for the 51 static face landmarks,
+    the dynamic-contour tables (79 bins x 17) and the flat_hand_mean=False
+    pose mean (55,3).
     """
     rng = np.random.default_rng(seed)
     V, J = num_verts, SMPLX_NUM_JOINTS
@@ -253,6 +255,15 @@ def synthetic_smplx_constants(seed: int = 1, num_verts: int = SMPLX_NUM_VERTS,
     c["lmk_bary_coords"] = (bc / bc.sum(axis=1, keepdims=True)).astype(np.float32)
     c["parents"] = SMPLX_PARENTS.copy()
     c["extra_verts"] = np.minimum(SMPLX_EXTRA_VERTS, V - 1).astype(np.int32)
+    # flat_hand_mean=False: the hand mean pose is added to the hand joints
+    pm = np.zeros((SMPLX_NUM_JOINTS, 3))
+    pm[25:] = rng.normal(0.0, 0.2, (30, 3))
+    c["pose_mean"] = pm.astype(np.float32)
+    # 17 dynamic face-contour landmarks, one (face, barycentric) set per
+    # y-rotation bin (79 bins: 0..39 and the negative-angle bins 40..78)
+    c["dynamic_lmk_faces_idx"] = rng.integers(0, num_faces, (79, 17)).astype(np.int32)
+    db = rng.uniform(0.05, 1.0, (79, 17, 3))
+    c["dynamic_lmk_bary_coords"] = (db / db.sum(axis=2, keepdims=True)).astype(np.float32)
     return c
 
 

@@ -64,6 +64,15 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
 /* Backbone only (StgGcn18.forward, st_gcn_aaai18.py:113-133): feat (N,T',V*Cout). */
 int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream);
 
+/* GEMM arithmetic: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
+ * 1 = 3-term f16 split (v_mfma_f32_16x16x32_f16 on x = hi + lo, fp32
+ * accumulate; ~2^-22 relative per product). Default 1, or 0 when the
+ * environment sets TIK_PRECISION=fp32 at handle creation. */
+#define TIK_PREC_F32 0
+#define TIK_PREC_F16X3 1
+int tik_model_set_precision(tik_model_t m, int prec);
+int tik_model_get_precision(tik_model_t m);
+
 /* Per-launch HIP-event profiling of the model's kernels (used by bench.py):
  * tik_model_profile(m, n) records up to n launches (0 disables, clears);
  * after synchronising, tik_model_profile_read returns launch i's label
@@ -86,6 +95,7 @@ int tik_block_create(const tik_tensor* tensors, int n_tensors, int in_channels, 
                      int stride, int residual, const float* A_eff_host, int V, tik_block_t* out);
 int tik_block_destroy(tik_block_t b);
 int tik_stgcn_block_fwd(tik_block_t b, const float* x, int N, int T, float* out, void* stream);
+int tik_block_set_precision(tik_block_t b, int prec);
 
 /* ------------------------------------------------------------------------
  * ConvTemporalGraphical.forward (gconv_origin.py:56-65), reference layout.
@@ -132,6 +142,7 @@ int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h
  * ---------------------------------------------------------------------- */
 int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t* out);
 int tik_fk_destroy(tik_fk_t fk);
+int tik_fk_set_precision(tik_fk_t fk, int prec);
 int tik_fk_num_joints(tik_fk_t fk);
 int tik_fk_num_verts(tik_fk_t fk);
 int tik_fk_reserve(tik_fk_t fk, int B);

@@ -38,6 +38,10 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_model_reserve": (_I, (_P, _I, _I)),
     "tik_ik_forward": (_I, (_P, _P, _I, _I, _P, _P)),
     "tik_backbone_forward": (_I, (_P, _P, _I, _I, _P, _P)),
+    "tik_model_set_precision": (_I, (_P, _I)),
+    "tik_model_get_precision": (_I, (_P,)),
+    "tik_block_set_precision": (_I, (_P, _I)),
+    "tik_fk_set_precision": (_I, (_P, _I)),
     "tik_model_profile": (_I, (_P, _I)),
     "tik_model_profile_count": (_I, (_P,)),
     "tik_model_profile_read": (_I, (_P, _I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_float),
@@ -74,6 +78,16 @@ def load(path: str = LIB_PATH):
         fn.argtypes = list(args)
     _lib = lib
     return lib
+
+
+PRECISIONS = {"fp32": 0, "f32": 0, "f16x3": 1}
+
+
+def precision_code(name: str) -> int:
+    """'fp32' = exact f32 MFMA, 'f16x3' = 3-term f16 split MFMA (see include/tik.h)."""
+    if name not in PRECISIONS:
+        raise ValueError(f"unknown precision {name!r}; expected one of {sorted(PRECISIONS)}")
+    return PRECISIONS[name]
 
 
 def last_error() -> str:

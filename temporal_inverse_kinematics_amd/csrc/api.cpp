@@ -32,6 +32,13 @@ namespace {
 
 int round4(int c) { return (c + 3) & ~3; }
 
+tik::Seg mkseg(const float* src, const float* w, const SplitW& sw, int cin, int ld, int kt, int stride, int pad,
+               int tin, int ldw) {
+    tik::Seg s{src, w, cin, ld, kt, stride, pad, tin, ldw};
+    s.whi = sw.hi.p; s.wlo = sw.lo.p; s.cin8 = sw.cin8; s.ldw8 = sw.ldw8;
+    return s;
+}
+
 // eval BatchNorm -> (scale, shift)
 int bn_fold(const TensorMap& m, const std::string& pre, int C, std::vector<float>& sc, std::vector<float>& sh) {
     const HostTensor* g = find(m, pre + ".weight");
@@ -105,13 +112,14 @@ struct ProfScope {
 
 // One StGcnBlock with BN folded into packed fp32 weights.
 struct Layer {
-    int cin = 0, cinp = 0, cout = 0, stride = 1, res = RES_IDEN, V = 17;
+    int cin = 0, cinp = 0, cout = 0, stride = 1, res = RES_IDEN, V = 17, index = 0;
     DevBuf wg;      // [cout][cinp]          gcn conv scaled by tcn.0 BN
     DevBuf bias2;   // [V][cout]             sc1*bg*colsum(A)[w] + sh1
     DevBuf amix;    // [V][V]                A_eff[v][w]
     DevBuf wt;      // [cout][3*cout]        tcn conv scaled by tcn.3 BN, k = tap*cout + ci
     DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
+    SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3)
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
               const std::vector<float>& A_eff, int V_) {
@@ -164,11 +172,12 @@ struct Layer {
                 for (int ci = 0; ci < cin; ++ci) hwr[(size_t)co * cinp + ci] = scr[co] * Wr->v[(size_t)co * cin + ci];
                 hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
             }
-            if ((rc = wr.upload(hwr))) return rc;
+            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp))) return rc;
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
         if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
-            (rc = biasT.upload(hbt)))
+            (rc = biasT.upload(hbt)) || (rc = swg.build(hwg, cout, 1, cinp, cinp)) ||
+            (rc = swt.build(hwt, cout, TK, cout, TK * cout)))
             return rc;
         return TIK_OK;
     }
@@ -177,26 +186,27 @@ struct Layer {
 
     // x: rows (N*tin*V) of ld floats (>= cinp, %4); z: workspace N*tin*V*cout;
     // out: rows (N*tout*V) of cout floats.
-    int forward(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st) const {
+    int forward(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st, int prec) const {
         const int to = tout(tin, stride);
         tik::CgemmArgs g{};
         g.M = N * tin * V; g.Nc = cout; g.V = V; g.tout = tin;
-        g.seg[0] = tik::Seg{x, wg.p, cinp, ld, 1, 1, 0, tin, cinp};
+        g.seg[0] = mkseg(x, wg.p, swg, cinp, ld, 1, 1, 0, tin, cinp);
         g.nseg = 1;
         g.bias = bias2.p; g.out = z; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
         const double px_in = (double)N * tin * V, px_out = (double)N * to * V;
         {
-            ProfScope p("G272x64.gcn_mix", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+            const std::string lab = "G272x64.L" + std::to_string(index);
+            ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
-            HIP_TRY(tik::launch_cgemm(g, tik::CFG_G272x64, st));
+            HIP_TRY(tik::launch_cgemm(g, tik::CFG_G272x64, st, prec));
         }
 
         tik::CgemmArgs t{};
         t.M = N * to * V; t.Nc = cout; t.V = V; t.tout = to;
-        t.seg[0] = tik::Seg{z, wt.p, cout, cout, TK, stride, 1, tin, TK * cout};
+        t.seg[0] = mkseg(z, wt.p, swt, cout, cout, TK, stride, 1, tin, TK * cout);
         t.nseg = 1;
         if (res == RES_CONV) {
-            t.seg[1] = tik::Seg{x, wr.p, cinp, ld, 1, stride, 0, tin, cinp};
+            t.seg[1] = mkseg(x, wr.p, swr, cinp, ld, 1, stride, 0, tin, cinp);
             t.nseg = 2;
         } else if (res == RES_IDEN) {
             t.resid = x; t.ldr = ld;
@@ -207,8 +217,9 @@ struct Layer {
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
         {
-            ProfScope p(big ? "T128x128.tcn_res" : "T128x64.tcn_res", fl, by, st);
-            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T128x64, st));
+            const std::string lab = std::string(big ? "T128x128.L" : "T128x64.L") + std::to_string(index);
+            ProfScope p(lab.c_str(), fl, by, st);
+            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T128x64, st, prec));
         }
         return TIK_OK;
     }
@@ -222,6 +233,8 @@ struct tik_model {
     std::vector<Layer> layers;
     DevBuf bn_sc, bn_sh;           // data_bn (V*C0)
     DevBuf w0, b0, w3, b3;         // head
+    SplitW sw0, sw3;
+    int prec = 1;
     DevBuf xb, z, a0, a1, hid;     // workspace
     Profiler prof;
     bool profiling = false;
@@ -235,6 +248,7 @@ struct ProfGuard {
 struct tik_block {
     Layer layer;
     DevBuf xp, z;   // padded-input and z workspace
+    int prec = 1;
 };
 
 extern "C" {
@@ -290,6 +304,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         std::vector<float> Ae(V * V);
         for (int i = 0; i < V * V; ++i) Ae[i] = A->v[i] * (imp ? imp->v[i] : 1.0f);
         md->layers.emplace_back();
+        md->layers.back().index = l;
         if ((rc = md->layers.back().build(m, pre, cin, cout, stride, 1, Ae, V))) { delete md; return rc; }
         cin = cout;
     }
@@ -304,7 +319,10 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     md->pose_dim = (int)W3->shape[0];
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
-    if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v))) {
+    md->prec = default_precision();
+    if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
+        (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
+        (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
         delete md;
         return rc;
     }
@@ -355,7 +373,7 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
     int which = 0;
     for (const Layer& L : m->layers) {
         float* o = bufs[which];
-        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st))) return rc;
+        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st, m->prec))) return rc;
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);
@@ -384,22 +402,39 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     const int rows = N * to;
     tik::CgemmArgs h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = tik::Seg{f, m->w0.p, m->feat, m->feat, 1, 1, 0, rows, m->feat};
+    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = m->hid.p; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
     {
         ProfScope pr("H64x128.head0", 2.0 * rows * m->feat * m->hidden,
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
-        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x128, st));
+        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x128, st, m->prec));
     }
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = tik::Seg{m->hid.p, m->w3.p, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden};
+    p.seg[0] = mkseg(m->hid.p, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
     {
         ProfScope pr("H64x128.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
-        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x128, st));
+        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x128, st, m->prec));
     }
+    return TIK_OK;
+}
+
+int tik_model_set_precision(tik_model_t m, int prec) {
+    if (!m || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_model_set_precision: bad arguments");
+    m->prec = prec;
+    return TIK_OK;
+}
+
+int tik_model_get_precision(tik_model_t m) {
+    if (!m) return fail(TIK_E_INVALID, "null model");
+    return m->prec;
+}
+
+int tik_block_set_precision(tik_block_t b, int prec) {
+    if (!b || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_block_set_precision: bad arguments");
+    b->prec = prec;
     return TIK_OK;
 }
 
@@ -437,6 +472,7 @@ int tik_block_create(const tik_tensor* tensors, int n_tensors, int in_channels, 
     TensorMap m = to_map(tensors, n_tensors);
     auto* b = new tik_block();
     std::vector<float> Ae(A_eff_host, A_eff_host + V * V);
+    b->prec = default_precision();
     int rc = b->layer.build(m, "", in_channels, out_channels, stride, residual, Ae, V);
     if (rc) { delete b; return rc; }
     *out = b;
@@ -461,7 +497,7 @@ int tik_stgcn_block_fwd(tik_block_t b, const float* x, int N, int T, float* out,
         xin = b->xp.p;
     }
     if ((rc = b->z.reserve(rows * L.cout))) return rc;
-    return L.forward(xin, L.cinp, N, T, b->z.p, out, st);
+    return L.forward(xin, L.cinp, N, T, b->z.p, out, st, b->prec);
 }
 
 // ---------------------------------------------------------------------------- ops

@@ -22,11 +22,15 @@ namespace tik {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
 enum { EPI_BIAS = 0, EPI_GRAPH = 1, EPI_SKIN = 2 };
+enum { PREC_F32 = 0, PREC_F16X3 = 1 };   // see cgemm.hip
 
 struct Seg {
     const float* src;   // rows of `ld` floats, cin used (cin % 4 == 0)
-    const float* w;     // [Nc][ldw], k = tap*cin + ci
+    const float* w;     // [Nc][ldw], k = tap*cin + ci                 (PREC_F32)
     int cin, ld, kt, stride, pad, tin, ldw;
+    const unsigned short* whi = nullptr;   // [Nc][ldw8] f16 bits, k = tap*cin8 + ci  (PREC_F16X3)
+    const unsigned short* wlo = nullptr;   // residual w - f16(w), same layout
+    int cin8 = 0, ldw8 = 0;                // cin rounded up to 8; row stride in halves
 };
 
 struct CgemmArgs {
@@ -52,6 +56,6 @@ enum CgemmCfg {
     CFG_S128x128 = 4,   // BM=128 (8 bodies x 16), BN=128 vertices, waves 2x2 : LBS skinning
 };
 
-hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st);
+hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec = PREC_F32);
 
 }  // namespace tik

@@ -1,32 +1,51 @@
-// cgemm.hip — implicit-GEMM temporal convolution on gfx950 fp32 MFMA
-// (v_mfma_f32_16x16x4_f32: exact f32 fma chain, 64 FLOP/clk/SIMD).
+// cgemm.hip — implicit-GEMM temporal convolution on gfx950 MFMA.
 //
 // Block = 256 threads = 4 waves; tile BM rows x BN output channels; K is
-// walked in chunks of 16 input channels per (segment, tap). Operands are
-// staged global -> registers -> LDS (double-buffered, one barrier per chunk),
-// A and B both stored [row][k] with a padded 20-float row so one
-// ds_read_b128 gives a lane 4 consecutive k. The 16x16x4 MFMA consumes them
-// k-permuted: MFMA step j takes k = {j, 4+j, 8+j, 12+j} from the four lane
-// groups, identically for A and B, so the sum is unchanged.
+// walked in chunks of BK input channels per (segment, tap). Operands are
+// staged global -> registers -> LDS (register prefetch of chunk i+1 while
+// chunk i computes), A and B both stored [row][k] in LDS with padded rows so
+// one ds_read_b128 feeds one MFMA operand. Two precisions:
+//
+//  PREC_F32   v_mfma_f32_16x16x4_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD).
+//             BK=16; the 4 k of a ds_read_b128 are consumed k-permuted: MFMA
+//             step j takes k = {j, 4+j, 8+j, 12+j} from the 4 lane groups,
+//             identically for A and B, so the sum is unchanged.
+//  PREC_F16X3 v_mfma_f32_16x16x32_f16 on a 2-term split of both operands,
+//             x = x_hi + x_lo (x_hi = f16(x), x_lo = f16(x - x_hi)), fp32
+//             accumulate of  a_lo.b_hi + a_hi.b_lo + a_hi.b_hi  (a_lo.b_lo,
+//             2^-22 relative, dropped): ~fp32 accuracy at 16/3 the f32-MFMA
+//             rate. BK=32. Activations are split when staged into LDS;
+//             weights arrive pre-split (host) as f16 pairs.
+//
+// Both share the C/D layout (lane holds rows 4*(lane>>4)+e, column lane&15),
+// hence the epilogues.
 #include "cgemm.h"
 
 namespace tik {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-static constexpr int BK = 16;
-static constexpr int LDK = 20;   // padded LDS row, floats (80 B, 16-B aligned)
+template <int PREC> struct PrecCfg;
+template <> struct PrecCfg<PREC_F32> { static constexpr int BK = 16, LDK = 20, ESZ = 4, PLANES = 1; };
+template <> struct PrecCfg<PREC_F16X3> { static constexpr int BK = 32, LDK = 40, ESZ = 2, PLANES = 2; };
 
-template <int BM, int BN, int WM, int WN, int EPI, int VT>
+template <int BM, int BN, int WM, int WN, int EPI, int VT, int PREC, int NBUF>
 __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     constexpr int FM = BM / WM / 16;
     constexpr int FN = BN / WN / 16;
     static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && WM * WN == 4, "tile");
-    constexpr int STAGE = 2 * (BM + BN) * LDK;
+    using PC = PrecCfg<PREC>;
+    constexpr int BK = PC::BK, LDK = PC::LDK;
+    // bytes of one staging buffer: (A planes + B planes) rows x LDK elements
+    constexpr int ROWB = LDK * PC::ESZ;
+    constexpr int BUFB = (BM + BN) * PC::PLANES * ROWB;
+    constexpr int STAGE = NBUF * BUFB;
     constexpr int LDC = BN + 1;
-    constexpr int CTILE = (EPI == EPI_GRAPH) ? BM * LDC : 0;
+    constexpr int CTILE = (EPI == EPI_GRAPH) ? BM * LDC * 4 : 0;
     constexpr int SMEM = STAGE > CTILE ? STAGE : CTILE;
-    __shared__ __attribute__((aligned(16))) float smem[SMEM];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -37,15 +56,21 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     const int V = (VT > 0) ? VT : a.V;
 
     // ---- per-thread staging assignment ---------------------------------
-    constexpr int NA4 = BM * 4, NB4 = BN * 4;   // float4 slots per chunk
-    constexpr int LA = (NA4 + 255) / 256, LB = (NB4 + 255) / 256;
+    // A: BM rows x BK fp32 = BM*KQ float4 slots (KQ = BK/4)
+    constexpr int KQ = BK / 4;
+    constexpr int NA4 = BM * KQ;
+    constexpr int LA = (NA4 + 255) / 256;
+    // B: F32: BN*KQ float4 slots; F16X3: BN*(2*BK/8) 16-B slots (hi and lo planes)
+    constexpr int BQ = (PREC == PREC_F32) ? KQ : 2 * BK / 8;
+    constexpr int NB4 = BN * BQ;
+    constexpr int LB = (NB4 + 255) / 256;
     int a_q[LA], a_lrow[LA], a_n[LA], a_t[LA], a_w[LA];
     bool a_live[LA];
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
         const int idx = tid + i * 256;
-        a_lrow[i] = idx >> 2;
-        a_q[i] = idx & 3;
+        a_lrow[i] = idx / KQ;
+        a_q[i] = idx % KQ;
         const int r = r0 + a_lrow[i];
         a_live[i] = (idx < NA4) && (r < a.M);
         const int rr = a_live[i] ? r : 0;
@@ -59,12 +84,11 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
         const int idx = tid + i * 256;
-        b_lrow[i] = idx >> 2;
-        b_q[i] = idx & 3;
+        b_lrow[i] = idx / BQ;
+        b_q[i] = idx % BQ;
         b_live[i] = (idx < NB4) && (n0 + b_lrow[i] < a.Nc);
     }
 
-    // ---- chunk schedule: (seg, tap, c0) ---------------------------------
     int nchunk = 0;
     for (int s = 0; s < a.nseg; ++s) nchunk += a.seg[s].kt * ((a.seg[s].cin + BK - 1) / BK);
 
@@ -85,24 +109,57 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int c = c0 + 4 * b_q[i];
-            if (b_live[i] && c < sg.cin)
-                v = *reinterpret_cast<const f32x4*>(sg.w + (size_t)(n0 + b_lrow[i]) * sg.ldw +
-                                                    tap * sg.cin + c);
+            if constexpr (PREC == PREC_F32) {
+                const int c = c0 + 4 * b_q[i];
+                if (b_live[i] && c < sg.cin)
+                    v = *reinterpret_cast<const f32x4*>(sg.w + (size_t)(n0 + b_lrow[i]) * sg.ldw + tap * sg.cin + c);
+            } else {
+                const int part = b_q[i] & 3;
+                const int c = c0 + 8 * part;
+                if (b_live[i] && c < sg.cin8) {
+                    const unsigned short* base = (b_q[i] < 4) ? sg.whi : sg.wlo;
+                    v = *reinterpret_cast<const f32x4*>(base + (size_t)(n0 + b_lrow[i]) * sg.ldw8 + tap * sg.cin8 + c);
+                }
+            }
             rb[i] = v;
         }
     };
     auto store_chunk = [&](int buf) {
-        float* As = smem + buf * (BM + BN) * LDK;
-        float* Bs = As + BM * LDK;
+        unsigned char* base = smem + buf * BUFB;
+        if constexpr (PREC == PREC_F32) {
+            float* As = reinterpret_cast<float*>(base);
+            float* Bs = As + BM * LDK;
 #pragma unroll
-        for (int i = 0; i < LA; ++i)
-            if (tid + i * 256 < NA4)
-                *reinterpret_cast<f32x4*>(As + a_lrow[i] * LDK + 4 * a_q[i]) = ra[i];
+            for (int i = 0; i < LA; ++i)
+                if (tid + i * 256 < NA4) *reinterpret_cast<f32x4*>(As + a_lrow[i] * LDK + 4 * a_q[i]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < LB; ++i)
-            if (tid + i * 256 < NB4)
-                *reinterpret_cast<f32x4*>(Bs + b_lrow[i] * LDK + 4 * b_q[i]) = rb[i];
+            for (int i = 0; i < LB; ++i)
+                if (tid + i * 256 < NB4) *reinterpret_cast<f32x4*>(Bs + b_lrow[i] * LDK + 4 * b_q[i]) = rb[i];
+        } else {
+            _Float16* Ahi = reinterpret_cast<_Float16*>(base);
+            _Float16* Alo = Ahi + BM * LDK;
+            _Float16* Bhi = Alo + BM * LDK;
+            _Float16* Blo = Bhi + BN * LDK;
+#pragma unroll
+            for (int i = 0; i < LA; ++i)
+                if (tid + i * 256 < NA4) {
+                    const f32x4 x = ra[i];
+                    f16x4 h, l;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        h[e] = (_Float16)x[e];
+                        l[e] = (_Float16)(x[e] - (float)h[e]);
+                    }
+                    *reinterpret_cast<f16x4*>(Ahi + a_lrow[i] * LDK + 4 * a_q[i]) = h;
+                    *reinterpret_cast<f16x4*>(Alo + a_lrow[i] * LDK + 4 * a_q[i]) = l;
+                }
+#pragma unroll
+            for (int i = 0; i < LB; ++i)
+                if (tid + i * 256 < NB4) {
+                    _Float16* dst = (b_q[i] < 4) ? Bhi : Blo;
+                    *reinterpret_cast<f32x4*>(dst + b_lrow[i] * LDK + 8 * (b_q[i] & 3)) = rb[i];
+                }
+        }
     };
 
     f32x4 acc[FM][FN];
@@ -110,6 +167,52 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int arow = wm * FM * 16 + (lane & 15);
+    const int brow = wn * FN * 16 + (lane & 15);
+    auto compute = [&](int buf) {
+        const unsigned char* base = smem + buf * BUFB;
+        if constexpr (PREC == PREC_F32) {
+            const float* As = reinterpret_cast<const float*>(base);
+            const float* Bs = As + BM * LDK;
+            const int kof = 4 * (lane >> 4);
+            f32x4 fb[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const f32x4*>(Bs + (brow + j * 16) * LDK + kof);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const f32x4 fa = *reinterpret_cast<const f32x4*>(As + (arow + i * 16) * LDK + kof);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[k], fb[j][k], acc[i][j], 0, 0, 0);
+            }
+        } else {
+            const _Float16* Ahi = reinterpret_cast<const _Float16*>(base);
+            const _Float16* Alo = Ahi + BM * LDK;
+            const _Float16* Bhi = Alo + BM * LDK;
+            const _Float16* Blo = Bhi + BN * LDK;
+            const int kof = 8 * (lane >> 4);
+            f16x8 bh[FN], bl[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                bh[j] = *reinterpret_cast<const f16x8*>(Bhi + (brow + j * 16) * LDK + kof);
+                bl[j] = *reinterpret_cast<const f16x8*>(Blo + (brow + j * 16) * LDK + kof);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + (arow + i * 16) * LDK + kof);
+                const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + (arow + i * 16) * LDK + kof);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    };
 
     int seg = 0, tap = 0, c0 = 0;
     auto advance = [&]() {
@@ -121,36 +224,31 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     };
 
     load_chunk(seg, tap, c0);
-    store_chunk(0);
-    __syncthreads();
-    const int arow = wm * FM * 16 + (lane & 15);
-    const int brow = wn * FN * 16 + (lane & 15);
-    const int kof = 4 * (lane >> 4);
-    for (int ch = 0; ch < nchunk; ++ch) {
-        const int buf = ch & 1;
-        const bool more = ch + 1 < nchunk;
-        if (more) {
-            advance();
-            load_chunk(seg, tap, c0);
-        }
-        const float* As = smem + buf * (BM + BN) * LDK;
-        const float* Bs = As + BM * LDK;
-        f32x4 fa[FM], fb[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-            fa[i] = *reinterpret_cast<const f32x4*>(As + (arow + i * 16) * LDK + kof);
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-            fb[j] = *reinterpret_cast<const f32x4*>(Bs + (brow + j * 16) * LDK + kof);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][k], fb[j][k], acc[i][j], 0, 0, 0);
-        if (more) store_chunk(buf ^ 1);
+    if constexpr (NBUF == 2) {
+        store_chunk(0);
         __syncthreads();
+        for (int ch = 0; ch < nchunk; ++ch) {
+            const int buf = ch & 1;
+            const bool more = ch + 1 < nchunk;
+            if (more) {
+                advance();
+                load_chunk(seg, tap, c0);
+            }
+            compute(buf);
+            if (more) store_chunk(buf ^ 1);
+            __syncthreads();
+        }
+    } else {
+        for (int ch = 0; ch < nchunk; ++ch) {
+            store_chunk(0);
+            __syncthreads();
+            if (ch + 1 < nchunk) {
+                advance();
+                load_chunk(seg, tap, c0);
+            }
+            compute(0);
+            __syncthreads();
+        }
     }
 
     // ---- epilogue ---------------------------------------------------------
@@ -200,7 +298,7 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         }
     } else {
         // graph epilogue: BM = F frames * V joints, frame-aligned tiles.
-        float* Cs = smem;
+        float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -235,41 +333,35 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     }
 }
 
-hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st) {
+template <int BM, int BN, int WM, int WN, int EPI, int VT>
+static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
+    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(256);
+    // the graph tile (BM=272) keeps one staging buffer in f16x3 so that two
+    // workgroups fit a CU's 160 KiB of LDS
+    constexpr int NB16 = (BM > 128) ? 1 : 2;
+    if (prec == PREC_F16X3)
+        hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F16X3, NB16>), g, blk, 0, st, a);
+    else
+        hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F32, 2>), g, blk, 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
-    const dim3 blk(256);
+    if (prec == PREC_F16X3)
+        for (int s = 0; s < a.nseg; ++s)
+            if (!a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
     (void)hipGetLastError();   // drop a stale error left by earlier runtime calls (not ours)
     switch (cfg) {
-        case CFG_T128x128: {
-            dim3 g((a.M + 127) / 128, (a.Nc + 127) / 128);
-            hipLaunchKernelGGL((cgemm_kernel<128, 128, 2, 2, EPI_BIAS, 0>), g, blk, 0, st, a);
-            break;
-        }
-        case CFG_T128x64: {
-            dim3 g((a.M + 127) / 128, (a.Nc + 63) / 64);
-            hipLaunchKernelGGL((cgemm_kernel<128, 64, 2, 2, EPI_BIAS, 0>), g, blk, 0, st, a);
-            break;
-        }
-        case CFG_G272x64: {
+        case CFG_T128x128: return launch_t<128, 128, 2, 2, EPI_BIAS, 0>(a, prec, st);
+        case CFG_T128x64: return launch_t<128, 64, 2, 2, EPI_BIAS, 0>(a, prec, st);
+        case CFG_G272x64:
             if (a.V != 17) return hipErrorInvalidValue;
-            dim3 g((a.M + 271) / 272, (a.Nc + 63) / 64);
-            hipLaunchKernelGGL((cgemm_kernel<272, 64, 1, 4, EPI_GRAPH, 17>), g, blk, 0, st, a);
-            break;
-        }
-        case CFG_S128x128: {
-            dim3 g((a.M + 127) / 128, (a.Nc + 127) / 128);
-            hipLaunchKernelGGL((cgemm_kernel<128, 128, 2, 2, EPI_SKIN, 0>), g, blk, 0, st, a);
-            break;
-        }
-        case CFG_H64x128: {
-            dim3 g((a.M + 63) / 64, (a.Nc + 127) / 128);
-            hipLaunchKernelGGL((cgemm_kernel<64, 128, 2, 2, EPI_BIAS, 0>), g, blk, 0, st, a);
-            break;
-        }
-        default:
-            return hipErrorInvalidValue;
+            return launch_t<272, 64, 1, 4, EPI_GRAPH, 17>(a, prec, st);
+        case CFG_H64x128: return launch_t<64, 128, 2, 2, EPI_BIAS, 0>(a, prec, st);
+        case CFG_S128x128: return launch_t<128, 128, 2, 2, EPI_SKIN, 0>(a, prec, st);
+        default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace tik

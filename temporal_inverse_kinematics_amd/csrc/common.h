@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <vector>
@@ -100,6 +101,39 @@ struct DevArray {   // owning device buffer; move-only (a copy would double-free
 };
 using DevBuf = DevArray<float>;
 using DevIBuf = DevArray<int>;
+using DevHBuf = DevArray<unsigned short>;
+
+// fp32 weights [Nc][kt][cin] (row stride ldw floats) -> f16 hi/lo planes
+// [Nc][kt][cin8] (cin8 = cin rounded up to 8, zero-filled): w = hi + lo with
+// hi = f16(w), lo = f16(w - hi) (round-to-nearest-even both times).
+struct SplitW {
+    DevHBuf hi, lo;
+    int cin8 = 0, ldw8 = 0;
+    int build(const std::vector<float>& w, int Nc, int kt, int cin, int ldw) {
+        cin8 = (cin + 7) & ~7;
+        ldw8 = kt * cin8;
+        std::vector<unsigned short> h((size_t)Nc * ldw8, 0), l((size_t)Nc * ldw8, 0);
+        for (int n = 0; n < Nc; ++n)
+            for (int t = 0; t < kt; ++t)
+                for (int c = 0; c < cin; ++c) {
+                    const float x = w[(size_t)n * ldw + (size_t)t * cin + c];
+                    const _Float16 xh = (_Float16)x;
+                    const _Float16 xl = (_Float16)(x - (float)xh);
+                    h[(size_t)n * ldw8 + (size_t)t * cin8 + c] = __builtin_bit_cast(unsigned short, xh);
+                    l[(size_t)n * ldw8 + (size_t)t * cin8 + c] = __builtin_bit_cast(unsigned short, xl);
+                }
+        int rc;
+        if ((rc = hi.upload(h)) || (rc = lo.upload(l))) return rc;
+        return TIK_OK;
+    }
+};
+
+// default arithmetic of the GEMMs: TIK_PRECISION=fp32 selects the exact f32
+// MFMA path; anything else the 3-term f16 split (cgemm.hip)
+inline int default_precision() {
+    const char* e = getenv("TIK_PRECISION");
+    return (e && (std::string(e) == "fp32" || std::string(e) == "f32")) ? 0 : 1;
+}
 
 
 }  // namespace tik_host

@@ -30,6 +30,8 @@ struct tik_fk {
     bool contour = false;
     DevBuf PT;         // [3V][KP]
     DevBuf WT;         // [V][KJ]
+    SplitW sPT, sWT;   // f16 hi/lo planes (PREC_F16X3)
+    int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
     DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra;
     int nchain = 0;
@@ -149,7 +151,9 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         if ((int)pm->v.size() != NJ * 3) return bad("pose_mean must be (55,3)");
         hpm = pm->v;
     }
-    if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
+    fk->prec = default_precision();
+    if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->sPT.build(PT, 3 * V, 1, KP, KP)) ||
+        (rc = fk->sWT.build(WT, V, 1, KJ, KJ)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
         (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
         (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||
         (rc = fk->extra.upload(hex))) {
@@ -166,6 +170,12 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
 
 int tik_fk_destroy(tik_fk_t fk) {
     delete fk;
+    return TIK_OK;
+}
+
+int tik_fk_set_precision(tik_fk_t fk, int prec) {
+    if (!fk || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_fk_set_precision: bad arguments");
+    fk->prec = prec;
     return TIK_OK;
 }
 
@@ -212,14 +222,16 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     tik::CgemmArgs g{};   // v_posed = feat . P
     g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
     g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
+    g.seg[0].whi = fk->sPT.hi.p; g.seg[0].wlo = fk->sPT.lo.p; g.seg[0].cin8 = fk->sPT.cin8; g.seg[0].ldw8 = fk->sPT.ldw8;
     g.nseg = 1; g.out = fk->vposed.p; g.ldo = V3; g.act = tik::ACT_NONE;
-    HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st));
+    HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
 
     tik::CgemmArgs s{};   // skinning + vertex transform
     s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
     s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
+    s.seg[0].whi = fk->sWT.hi.p; s.seg[0].wlo = fk->sWT.lo.p; s.seg[0].cin8 = fk->sWT.cin8; s.seg[0].ldw8 = fk->sWT.ldw8;
     s.nseg = 1; s.resid = fk->vposed.p; s.ldr = V3; s.out = vout; s.ldo = V3; s.bias = transl;
-    HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st));
+    HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
 
     tik::FkLmkArgs l{};
     l.B = B; l.V = fk->V; l.njoints = fk->njoints; l.nextra = fk->nextra; l.nlmk = fk->nlmk; l.ndyn = fk->ndyn;

@@ -40,13 +40,14 @@ def run_inference(model, seq_3d_kps: np.ndarray) -> np.ndarray:
     return out
 
 
-def synthetic_model(win_size: int = 64, device="cuda", seed: int = 0):
+def synthetic_model(win_size: int = 64, device="cuda", seed: int = 0, precision=None):
     """IKPoseTrainer with the seeded synthetic weights of synthetic.ik_state_dict."""
     from . import synthetic as syn
     from .models import IKPoseTrainer, default_hparams
     model = IKPoseTrainer(default_hparams(win_size))
     sd = syn.ik_state_dict(model.regressor.backbone.graph.A, seed=seed)
     model.regressor.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    model.regressor.tik_precision = precision
     return model.to(device).eval()
 
 

@@ -105,6 +105,7 @@ class StGcnBlock(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self._tik = None
         self._tik_key = None
+        self.tik_precision = None
 
     def _handle(self, A: torch.Tensor):
         if self.training:
@@ -124,6 +125,8 @@ class StGcnBlock(nn.Module):
                        "StGcnBlock")
             self._tik = _Handle(h.value, lib.tik_block_destroy)
             self._tik_key = key
+        if self.tik_precision is not None:
+            _lib.check(_lib.load().tik_block_set_precision(self._tik.h, _lib.precision_code(self.tik_precision)))
         return self._tik.h
 
     def forward(self, x, A):
@@ -192,6 +195,7 @@ class PoseRegressor(nn.Module):
                                             nn.Linear(512, self.pose_dim))
         self._tik = None
         self._tik_key = None
+        self.tik_precision = None   # None: library default; "fp32" | "f16x3"
 
     def tik_handle(self):
         """The libtik model handle for the current weights (rebuilt when they change)."""
@@ -207,6 +211,8 @@ class PoseRegressor(nn.Module):
             _lib.check(lib.tik_model_create(arr, len(named), _lib.ctypes.byref(h)), "PoseRegressor")
             self._tik = _Handle(h.value, lib.tik_model_destroy)
             self._tik_key = key
+        if self.tik_precision is not None:
+            _lib.check(_lib.load().tik_model_set_precision(self._tik.h, _lib.precision_code(self.tik_precision)))
         return self._tik.h
 
     def forward(self, x, init_pose=None, n_iter=3):

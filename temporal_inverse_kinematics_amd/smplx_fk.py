@@ -71,7 +71,7 @@ class SMPLX:
     NUM_BODY_JOINTS = 21
 
     def __init__(self, constants: Dict[str, np.ndarray], batch_size: int = 1, device="cuda",
-                 use_face_contour: bool = True, gender: str = "neutral"):
+                 use_face_contour: bool = True, gender: str = "neutral", precision: Optional[str] = None):
         self.batch_size = batch_size
         self.device = torch.device(device)
         self.gender = gender
@@ -85,6 +85,8 @@ class SMPLX:
         _lib.check(lib.tik_fk_create(arr, len(named), int(use_face_contour), _lib.ctypes.byref(h)), "SMPLX")
         self._h = h.value
         self._destroy = lib.tik_fk_destroy
+        if precision is not None:
+            _lib.check(lib.tik_fk_set_precision(self._h, _lib.precision_code(precision)))
         self.num_joints = _lib.check(lib.tik_fk_num_joints(self._h))
         self.num_verts = _lib.check(lib.tik_fk_num_verts(self._h))
 

@@ -19,10 +19,10 @@ def consts():
     return syn.synthetic_smplx_constants(seed=1)
 
 
-@pytest.fixture(scope="module")
-def model(consts):
+@pytest.fixture(scope="module", params=["fp32", "f16x3"])
+def model(consts, request):
     from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
-    return SMPLX(consts, batch_size=9)
+    return SMPLX(consts, batch_size=9, precision=request.param)
 
 
 def _inputs(B, seed):

@@ -13,12 +13,12 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module")
-def model():
+@pytest.fixture(scope="module", params=["fp32", "f16x3"])
+def model(request):
     from temporal_inverse_kinematics_amd import _build
     _build.build()
     from temporal_inverse_kinematics_amd.inference import synthetic_model
-    return synthetic_model(win_size=64, device="cuda")
+    return synthetic_model(win_size=64, device="cuda", precision=request.param)
 
 
 @pytest.fixture(scope="module")
@@ -74,12 +74,13 @@ def test_run_inference_sample(model):
     y64 = run_inference(model, r["seq"])
     assert y64.dtype == np.float32 and y64.shape == (231, 66)
     assert np.abs(y64 - r["win64"]).max() < TOL
-    m9 = synthetic_model(win_size=9, device="cuda")
+    m9 = synthetic_model(win_size=9, device="cuda", precision=model.regressor.tik_precision)
     y9 = run_inference(m9, r["seq"])
     assert np.abs(y9 - r["win9"]).max() < TOL
 
 
-def test_blocks_vs_golden():
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_blocks_vs_golden(prec):
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.models import StGcnBlock
     b = golden("blocks.npz")
@@ -89,6 +90,7 @@ def test_blocks_vs_golden():
         sdb = syn.block_state_dict("", cin, cout, s, residual=bool(residual), seed=5)
         blk.load_state_dict({k: torch.from_numpy(v) for k, v in sdb.items()}, strict=False)
         blk = blk.cuda().eval()
+        blk.tik_precision = prec
         A = torch.from_numpy(b["A"] * b[f"{tag}|imp"]).cuda()
         for T in [9, 16]:
             with torch.no_grad():

@@ -124,6 +124,22 @@ int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h
                       int root_b, int relative, float* windows, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Online IK (BASELINE.json config #5): stride-1 sliding window over a live
+ * sequence. tik_stream_push copies one frame (V=17 x 3 host floats) into a
+ * device ring, gathers the window centred h = win_size/2 frames back (left
+ * edge clamped as data_amass.py:18-42), runs the IK forward (N=1) and returns
+ * pose row 0 (66 floats) — identical to inference.run_inference's frame
+ * (inference.py:37-67). Returns 1 when a pose was produced (after h+1 pushes),
+ * 0 before, <0 on error. The step is one hipGraph replay when use_graph != 0.
+ * Flush the last h frames by pushing the last frame h more times.
+ * ---------------------------------------------------------------------- */
+typedef struct tik_stream* tik_stream_t;
+int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream_t* out);
+int tik_stream_destroy(tik_stream_t s);
+int tik_stream_reset(tik_stream_t s);
+int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host);
+
+/* ------------------------------------------------------------------------
  * SMPL-X forward kinematics + linear blend skinning (the FK check).
  * Replaces common/smpl_util.py:8-82 (load_smplx_models / run_smpl_inference)
  * and the third-party smplx.SMPLX.forward it calls (smpl_util.py:67-69;

@@ -120,6 +120,7 @@ struct Layer {
     DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
     SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3)
+    bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
               const std::vector<float>& A_eff, int V_) {
@@ -175,6 +176,7 @@ struct Layer {
             if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp))) return rc;
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
+        mix_sparse = tik::fits_coco_hop2(ha.data(), V);
         if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
             (rc = biasT.upload(hbt)) || (rc = swg.build(hwg, cout, 1, cinp, cinp)) ||
             (rc = swt.build(hwt, cout, TK, cout, TK * cout)))
@@ -193,6 +195,7 @@ struct Layer {
         g.seg[0] = mkseg(x, wg.p, swg, cinp, ld, 1, 1, 0, tin, cinp);
         g.nseg = 1;
         g.bias = bias2.p; g.out = z; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
+        g.mix_sparse = mix_sparse ? 1 : 0;
         const double px_in = (double)N * tin * V, px_out = (double)N * to * V;
         {
             const std::string lab = "G272x64.L" + std::to_string(index);
@@ -217,9 +220,9 @@ struct Layer {
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
         {
-            const std::string lab = std::string(big ? "T128x128.L" : "T128x64.L") + std::to_string(index);
+            const std::string lab = std::string(big ? "T128x128.L" : "T256x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
-            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T128x64, st, prec));
+            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T256x64, st, prec));
         }
         return TIK_OK;
     }
@@ -405,18 +408,18 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = m->hid.p; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
     {
-        ProfScope pr("H64x128.head0", 2.0 * rows * m->feat * m->hidden,
+        ProfScope pr("H64x64.head0", 2.0 * rows * m->feat * m->hidden,
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
-        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x128, st, m->prec));
+        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x64, st, m->prec));
     }
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
     p.seg[0] = mkseg(m->hid.p, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
     {
-        ProfScope pr("H64x128.head3", 2.0 * rows * m->hidden * m->pose_dim,
+        ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
-        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x128, st, m->prec));
+        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x64, st, m->prec));
     }
     return TIK_OK;
 }

@@ -44,6 +44,7 @@ struct CgemmArgs {
     int ldo;
     const float* amix;   // EPI_GRAPH: [V][V], A_eff[v][w]
     int act;
+    int mix_sparse = 0;  // EPI_GRAPH: A_eff's nonzeros lie inside the COCO hop<=2 pattern
     // EPI_SKIN: resid = v_posed [B][ldr], out = verts [B][ldo], bias = transl [B][3] or null
 };
 
@@ -54,7 +55,13 @@ enum CgemmCfg {
     CFG_G272x64 = 2,    // BM=272 (16 frames x 17 joints), BN=64, waves 1x4 : gcn + V-mix
     CFG_H64x128 = 3,    // BM=64,  BN=128, waves 2x2 : head Linear layers
     CFG_S128x128 = 4,   // BM=128 (8 bodies x 16), BN=128 vertices, waves 2x2 : LBS skinning
+    CFG_T256x64 = 5,    // BM=256, BN=64,  waves 4x1 : tcn of 64-channel layers
+    CFG_H64x64 = 6,     // BM=64,  BN=64,  waves 2x2 : head (more workgroups)
 };
+
+// true when every nonzero of A (V x V, row-major A[v][w]) lies in the COCO-17
+// hop<=2 pattern the sparse graph epilogue unrolls
+bool fits_coco_hop2(const float* A, int V);
 
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec = PREC_F32);
 

@@ -3,8 +3,11 @@
 // Block = 256 threads = 4 waves; tile BM rows x BN output channels; K is
 // walked in chunks of BK input channels per (segment, tap). Operands are
 // staged global -> registers -> LDS (register prefetch of chunk i+1 while
-// chunk i computes), A and B both stored [row][k] in LDS with padded rows so
-// one ds_read_b128 feeds one MFMA operand. Two precisions:
+// chunk i computes), A and B both stored [row][k] in LDS as unpadded 64-B rows
+// of four 16-B chunks, chunk c of row r stored at c ^ SW[(r>>2)&3] with
+// SW = {0,3,2,1}: the 16-lane groups of a ds_read_b128 (lane l reads row l&15,
+// chunk l>>4) then hit 16 distinct 4-bank slots (conflict-free). One
+// ds_read_b128 feeds one MFMA operand. Two precisions:
 //
 //  PREC_F32   v_mfma_f32_16x16x4_f32 (exact f32 fma chain, 64 FLOP/clk/SIMD).
 //             BK=16; the 4 k of a ds_read_b128 are consumed k-permuted: MFMA
@@ -27,9 +30,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+// column w of the COCO-17 hop<=2 adjacency (Graph('coco','uniform',max_hop=2),
+// mmskeleton/ops/st_gcn/graph.py:76-133): bit v set <=> A[v][w] != 0 (107 entries)
+__host__ __device__ constexpr unsigned coco_hop2_mask(int w) {
+    constexpr unsigned m[17] = {0x1Fu,   0x3Fu,   0x5Fu,   0x8EFu,   0x1177u, 0x3BFAu, 0x5DFCu, 0xAE8u,  0x1570u,
+                                0x2A0u,  0x540u,  0xF8E8u, 0x17970u, 0xB820u, 0x15840u, 0xA800u, 0x15000u};
+    return m[w];
+}
+
 template <int PREC> struct PrecCfg;
-template <> struct PrecCfg<PREC_F32> { static constexpr int BK = 16, LDK = 20, ESZ = 4, PLANES = 1; };
-template <> struct PrecCfg<PREC_F16X3> { static constexpr int BK = 32, LDK = 40, ESZ = 2, PLANES = 2; };
+template <> struct PrecCfg<PREC_F32> { static constexpr int BK = 16, LDK = 16, ESZ = 4, PLANES = 1; };
+template <> struct PrecCfg<PREC_F16X3> { static constexpr int BK = 32, LDK = 32, ESZ = 2, PLANES = 2; };
+
+// byte offset of 16-B chunk c of 64-B row r in a swizzled [rows][64 B] image
+__device__ __forceinline__ int swz_off(int r, int c) { return r * 64 + ((c ^ ((0x1230 >> (4 * ((r >> 2) & 3))) & 3)) << 4); }
 
 template <int BM, int BN, int WM, int WN, int EPI, int VT, int PREC, int NBUF>
 __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
@@ -39,11 +53,12 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     using PC = PrecCfg<PREC>;
     constexpr int BK = PC::BK, LDK = PC::LDK;
     // bytes of one staging buffer: (A planes + B planes) rows x LDK elements
-    constexpr int ROWB = LDK * PC::ESZ;
+    constexpr int ROWB = 64;   // BK elements of ESZ bytes: 16 fp32 or 32 halves
+    static_assert(LDK * PC::ESZ == ROWB, "64-B rows");
     constexpr int BUFB = (BM + BN) * PC::PLANES * ROWB;
     constexpr int STAGE = NBUF * BUFB;
-    constexpr int LDC = BN + 1;
-    constexpr int CTILE = (EPI == EPI_GRAPH) ? BM * LDC * 4 : 0;
+    constexpr int LDC = BN + 4;   // fp32 C tile row (epilogue), 16-B aligned
+    constexpr int CTILE = (EPI == EPI_SKIN) ? 0 : BM * LDC * 4;
     constexpr int SMEM = STAGE > CTILE ? STAGE : CTILE;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
 
@@ -127,19 +142,19 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     auto store_chunk = [&](int buf) {
         unsigned char* base = smem + buf * BUFB;
         if constexpr (PREC == PREC_F32) {
-            float* As = reinterpret_cast<float*>(base);
-            float* Bs = As + BM * LDK;
+            unsigned char* As = base;
+            unsigned char* Bs = As + BM * 64;
 #pragma unroll
             for (int i = 0; i < LA; ++i)
-                if (tid + i * 256 < NA4) *reinterpret_cast<f32x4*>(As + a_lrow[i] * LDK + 4 * a_q[i]) = ra[i];
+                if (tid + i * 256 < NA4) *reinterpret_cast<f32x4*>(As + swz_off(a_lrow[i], a_q[i])) = ra[i];
 #pragma unroll
             for (int i = 0; i < LB; ++i)
-                if (tid + i * 256 < NB4) *reinterpret_cast<f32x4*>(Bs + b_lrow[i] * LDK + 4 * b_q[i]) = rb[i];
+                if (tid + i * 256 < NB4) *reinterpret_cast<f32x4*>(Bs + swz_off(b_lrow[i], b_q[i])) = rb[i];
         } else {
-            _Float16* Ahi = reinterpret_cast<_Float16*>(base);
-            _Float16* Alo = Ahi + BM * LDK;
-            _Float16* Bhi = Alo + BM * LDK;
-            _Float16* Blo = Bhi + BN * LDK;
+            unsigned char* Ahi = base;
+            unsigned char* Alo = Ahi + BM * 64;
+            unsigned char* Bhi = Alo + BM * 64;
+            unsigned char* Blo = Bhi + BN * 64;
 #pragma unroll
             for (int i = 0; i < LA; ++i)
                 if (tid + i * 256 < NA4) {
@@ -150,14 +165,16 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
                         h[e] = (_Float16)x[e];
                         l[e] = (_Float16)(x[e] - (float)h[e]);
                     }
-                    *reinterpret_cast<f16x4*>(Ahi + a_lrow[i] * LDK + 4 * a_q[i]) = h;
-                    *reinterpret_cast<f16x4*>(Alo + a_lrow[i] * LDK + 4 * a_q[i]) = l;
+                    // 4 fp32 channels 4q..4q+3 -> halves 4q..4q+3: chunk q>>1, +8 B when q is odd
+                    const int off = swz_off(a_lrow[i], a_q[i] >> 1) + 8 * (a_q[i] & 1);
+                    *reinterpret_cast<f16x4*>(Ahi + off) = h;
+                    *reinterpret_cast<f16x4*>(Alo + off) = l;
                 }
 #pragma unroll
             for (int i = 0; i < LB; ++i)
                 if (tid + i * 256 < NB4) {
-                    _Float16* dst = (b_q[i] < 4) ? Bhi : Blo;
-                    *reinterpret_cast<f32x4*>(dst + b_lrow[i] * LDK + 8 * (b_q[i] & 3)) = rb[i];
+                    unsigned char* dst = (b_q[i] < 4) ? Bhi : Blo;
+                    *reinterpret_cast<f32x4*>(dst + swz_off(b_lrow[i], b_q[i] & 3)) = rb[i];
                 }
         }
     };
@@ -172,16 +189,16 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     const int brow = wn * FN * 16 + (lane & 15);
     auto compute = [&](int buf) {
         const unsigned char* base = smem + buf * BUFB;
+        const int g = lane >> 4;
         if constexpr (PREC == PREC_F32) {
-            const float* As = reinterpret_cast<const float*>(base);
-            const float* Bs = As + BM * LDK;
-            const int kof = 4 * (lane >> 4);
+            const unsigned char* As = base;
+            const unsigned char* Bs = As + BM * 64;
             f32x4 fb[FN];
 #pragma unroll
-            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const f32x4*>(Bs + (brow + j * 16) * LDK + kof);
+            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const f32x4*>(Bs + swz_off(brow + j * 16, g));
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const f32x4 fa = *reinterpret_cast<const f32x4*>(As + (arow + i * 16) * LDK + kof);
+                const f32x4 fa = *reinterpret_cast<const f32x4*>(As + swz_off(arow + i * 16, g));
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -189,21 +206,22 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[k], fb[j][k], acc[i][j], 0, 0, 0);
             }
         } else {
-            const _Float16* Ahi = reinterpret_cast<const _Float16*>(base);
-            const _Float16* Alo = Ahi + BM * LDK;
-            const _Float16* Bhi = Alo + BM * LDK;
-            const _Float16* Blo = Bhi + BN * LDK;
-            const int kof = 8 * (lane >> 4);
+            const unsigned char* Ahi = base;
+            const unsigned char* Alo = Ahi + BM * 64;
+            const unsigned char* Bhi = Alo + BM * 64;
+            const unsigned char* Blo = Bhi + BN * 64;
             f16x8 bh[FN], bl[FN];
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
-                bh[j] = *reinterpret_cast<const f16x8*>(Bhi + (brow + j * 16) * LDK + kof);
-                bl[j] = *reinterpret_cast<const f16x8*>(Blo + (brow + j * 16) * LDK + kof);
+                const int off = swz_off(brow + j * 16, g);
+                bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
+                bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
             }
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + (arow + i * 16) * LDK + kof);
-                const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + (arow + i * 16) * LDK + kof);
+                const int off = swz_off(arow + i * 16, g);
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
+                const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
@@ -256,23 +274,42 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
     const int ccol0 = wn * FN * 16 + (lane & 15);
     if constexpr (EPI == EPI_BIAS) {
+        // acc -> LDS C tile -> row-contiguous float4 epilogue (bias, residual, act)
+        float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int col = n0 + ccol0 + j * 16;
-            if (col >= a.Nc) continue;
-            const float bj = a.bias ? a.bias[col] : 0.f;
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
+        __syncthreads();
+        constexpr int C4 = BN / 4;
+        const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0);
+        for (int p = tid; p < BM * C4; p += 256) {
+            const int lr = p / C4, c4 = p % C4;
+            const int row = r0 + lr, col = n0 + 4 * c4;
+            if (row >= a.M || col >= a.Nc) continue;
+            const f32x4 cv = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4);
+            if (vec && col + 3 < a.Nc) {
+                f32x4 v = cv;
+                if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + col);
+                if (a.resid) v += *reinterpret_cast<const f32x4*>(a.resid + (size_t)row * a.ldr + col);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int row = r0 + crow0 + i * 16 + e;
-                    if (row >= a.M) continue;
-                    float v = acc[i][j][e] + bj;
-                    if (a.resid) v += a.resid[(size_t)row * a.ldr + col];
+                    if (a.act == ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    else if (a.act == ACT_LEAKY) v[e] = v[e] > 0.f ? v[e] : 0.01f * v[e];
+                }
+                *reinterpret_cast<f32x4*>(a.out + (size_t)row * a.ldo + col) = v;
+            } else {
+                for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                    float v = cv[e] + (a.bias ? a.bias[col + e] : 0.f);
+                    if (a.resid) v += a.resid[(size_t)row * a.ldr + col + e];
                     if (a.act == ACT_RELU) v = v > 0.f ? v : 0.f;
                     else if (a.act == ACT_LEAKY) v = v > 0.f ? v : 0.01f * v;
-                    a.out[(size_t)row * a.ldo + col] = v;
+                    a.out[(size_t)row * a.ldo + col + e] = v;
                 }
+            }
         }
     } else if constexpr (EPI == EPI_SKIN) {
         // rows r = b*16 + e, e = 4*row + col of the 3x4 transform T_v(b); lane
@@ -297,7 +334,12 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
             }
         }
     } else {
-        // graph epilogue: BM = F frames * V joints, frame-aligned tiles.
+        // graph epilogue: BM = F frames * V joints, frame-aligned tiles. One
+        // thread per (frame, 4 channels): y[v] for the 17 joints from LDS,
+        // z[w] = sum_v A[v][w] y[v] over the COCO hop<=2 pattern (107 of 289
+        // entries, unrolled at compile time) when the layer's A fits it,
+        // else dense; + bias2[w][c]; ReLU; float4 stores.
+        static_assert(VT == 17 && BN % 4 == 0, "graph epilogue is built for the 17-joint COCO graph");
         float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -307,27 +349,42 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
                 for (int e = 0; e < 4; ++e)
                     Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
         __syncthreads();
-        static_assert(VT > 0 && BM % VT == 0, "graph epilogue needs whole frames");
         constexpr int FR = BM / VT;
-        constexpr int PAIRS = FR * BN;
+        constexpr int C4 = BN / 4;
         const int frame0 = r0 / VT;
         const int nframes = a.M / VT;
-        for (int p = tid; p < PAIRS; p += 256) {
-            const int c = p % BN;
-            const int f = p / BN;
-            const int col = n0 + c;
+        for (int p = tid; p < FR * C4; p += 256) {
+            const int c4 = p % C4;
+            const int f = p / C4;
+            const int col = n0 + 4 * c4;
             if (frame0 + f >= nframes || col >= a.Nc) continue;
-            float y[VT];
+            f32x4 y[VT];
 #pragma unroll
-            for (int v = 0; v < VT; ++v) y[v] = Cs[(f * VT + v) * LDC + c];
+            for (int v = 0; v < VT; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * VT + v) * LDC + 4 * c4);
             float* o = a.out + (size_t)(frame0 + f) * VT * a.ldo + col;
+            const bool full = col + 3 < a.Nc;
 #pragma unroll
             for (int w = 0; w < VT; ++w) {
-                float z = 0.f;
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                if (a.mix_sparse) {
 #pragma unroll
-                for (int v = 0; v < VT; ++v) z = fmaf(a.amix[v * VT + w], y[v], z);
-                z += a.bias[w * a.Nc + col];
-                o[(size_t)w * a.ldo] = z > 0.f ? z : 0.f;
+                    for (int v = 0; v < VT; ++v)
+                        if ((coco_hop2_mask(w) >> v) & 1u) z += a.amix[v * VT + w] * y[v];
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VT; ++v) z += a.amix[v * VT + w] * y[v];
+                }
+                if (full) {
+                    z += *reinterpret_cast<const f32x4*>(a.bias + w * a.Nc + col);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                    *reinterpret_cast<f32x4*>(o + (size_t)w * a.ldo) = z;
+                } else {
+                    for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                        const float t = z[e] + a.bias[w * a.Nc + col + e];
+                        o[(size_t)w * a.ldo + e] = t > 0.f ? t : 0.f;
+                    }
+                }
             }
         }
     }
@@ -338,12 +395,20 @@ static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
     const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(256);
     // the graph tile (BM=272) keeps one staging buffer in f16x3 so that two
     // workgroups fit a CU's 160 KiB of LDS
-    constexpr int NB16 = (BM > 128) ? 1 : 2;
+    constexpr int NB16 = (EPI == EPI_GRAPH) ? 1 : 2;
     if (prec == PREC_F16X3)
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F16X3, NB16>), g, blk, 0, st, a);
     else
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F32, 2>), g, blk, 0, st, a);
     return hipGetLastError();
+}
+
+bool fits_coco_hop2(const float* A, int V) {
+    if (V != 17) return false;
+    for (int v = 0; v < 17; ++v)
+        for (int w = 0; w < 17; ++w)
+            if (A[v * 17 + w] != 0.f && !((coco_hop2_mask(w) >> v) & 1u)) return false;
+    return true;
 }
 
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
@@ -359,6 +424,8 @@ hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
             if (a.V != 17) return hipErrorInvalidValue;
             return launch_t<272, 64, 1, 4, EPI_GRAPH, 17>(a, prec, st);
         case CFG_H64x128: return launch_t<64, 128, 2, 2, EPI_BIAS, 0>(a, prec, st);
+        case CFG_T256x64: return launch_t<256, 64, 4, 1, EPI_BIAS, 0>(a, prec, st);
+        case CFG_H64x64: return launch_t<64, 64, 2, 2, EPI_BIAS, 0>(a, prec, st);
         case CFG_S128x128: return launch_t<128, 128, 2, 2, EPI_SKIN, 0>(a, prec, st);
         default: return hipErrorInvalidValue;
     }

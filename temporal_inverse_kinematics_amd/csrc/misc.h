@@ -14,4 +14,8 @@ hipError_t launch_gconv(const float* x, int N, int Cin, int T, int V, const floa
 
 hipError_t launch_pad_channels(const float* x, long long rows, int C, int Cp, float* y, hipStream_t st);
 
+hipError_t launch_stream_push(float* ring, int W, int nv, int* count, const float* frame, hipStream_t st);
+hipError_t launch_stream_window(const float* ring, int W, int V, const int* count, int h, int ra, int rb,
+                                int relative, float* out, hipStream_t st);
+
 }  // namespace tik

@@ -172,4 +172,50 @@ hipError_t launch_pad_channels(const float* x, long long rows, int C, int Cp, fl
     return hipGetLastError();
 }
 
+// ---- online (streaming) windowing: device ring of the last W = 2h+1 frames.
+// push: ring[count % W] = frame; ++count.  (one block)
+__global__ void stream_push_kernel(float* ring, int W, int nv, int* count, const float* frame) {
+    const int c = *count;
+    float* slot = ring + (size_t)(c % W) * nv;
+    for (int i = threadIdx.x; i < nv; i += blockDim.x) slot[i] = frame[i];
+    __syncthreads();
+    if (threadIdx.x == 0) *count = c + 1;
+}
+
+// window centred at c = count-1-h: frames c-h .. c+h = count-1-2h .. count-1,
+// each clamped to >= 0 (left edge padding of data_amass.py:30-33), root-relative.
+__global__ void stream_window_kernel(const float* ring, int W, int V, const int* count, int h, int ra, int rb,
+                                     int relative, float* out) {
+    const int n = *count;
+    const int last = n - 1;
+    for (int p = threadIdx.x; p < W * V; p += blockDim.x) {
+        const int k = p / V, v = p % V;
+        int f = last - 2 * h + k;
+        f = f < 0 ? 0 : f;
+        const float* fr = ring + (size_t)(f % W) * V * 3;
+        float o0 = fr[v * 3], o1 = fr[v * 3 + 1], o2 = fr[v * 3 + 2];
+        if (relative) {
+            o0 -= 0.5f * (fr[ra * 3] + fr[rb * 3]);
+            o1 -= 0.5f * (fr[ra * 3 + 1] + fr[rb * 3 + 1]);
+            o2 -= 0.5f * (fr[ra * 3 + 2] + fr[rb * 3 + 2]);
+        }
+        out[(size_t)p * 3] = o0;
+        out[(size_t)p * 3 + 1] = o1;
+        out[(size_t)p * 3 + 2] = o2;
+    }
+}
+
+hipError_t launch_stream_push(float* ring, int W, int nv, int* count, const float* frame, hipStream_t st) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(stream_push_kernel, dim3(1), dim3(64), 0, st, ring, W, nv, count, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_window(const float* ring, int W, int V, const int* count, int h, int ra, int rb,
+                                int relative, float* out, hipStream_t st) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(stream_window_kernel, dim3(1), dim3(256), 0, st, ring, W, V, count, h, ra, rb, relative, out);
+    return hipGetLastError();
+}
+
 }  // namespace tik

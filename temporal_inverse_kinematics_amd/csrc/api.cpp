@@ -220,9 +220,13 @@ struct Layer {
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
         {
-            const std::string lab = std::string(big ? "T128x128.L" : "T256x64.L") + std::to_string(index);
+            // 64-channel layers: 256x64 tiles for fp32; 128x64 for f16x3 (two register
+            // staging sets of a 256-row tile would cost a wave per SIMD)
+            const int cfg = big ? tik::CFG_T128x128 : (prec == tik::PREC_F32 ? tik::CFG_T256x64 : tik::CFG_T128x64);
+            const std::string lab = std::string(big ? "T128x128.L" : (cfg == tik::CFG_T256x64 ? "T256x64.L" : "T128x64.L")) +
+                                    std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
-            HIP_TRY(tik::launch_cgemm(t, big ? tik::CFG_T128x128 : tik::CFG_T256x64, st, prec));
+            HIP_TRY(tik::launch_cgemm(t, cfg, st, prec));
         }
         return TIK_OK;
     }

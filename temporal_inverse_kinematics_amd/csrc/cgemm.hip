@@ -107,39 +107,65 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     int nchunk = 0;
     for (int s = 0; s < a.nseg; ++s) nchunk += a.seg[s].kt * ((a.seg[s].cin + BK - 1) / BK);
 
-    f32x4 ra[LA], rb[LB];
-    auto load_chunk = [&](int seg, int tap, int c0) {
+    // Load cursor (seg, tap, c0) and per-thread source pointers for the current
+    // (seg, tap): row addresses are computed once per tap, not per chunk.
+    int seg = 0, tap = 0, c0 = 0;
+    const float* a_ptr[LA];
+    const unsigned char* b_ptr[LB];
+    int cin_cur = 0, bcin_cur = 0;
+    auto set_tap = [&]() {
         const Seg& sg = a.seg[seg];
+        cin_cur = sg.cin;
+#pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int t = sg.stride * a_t[i] + tap - sg.pad;
+            a_ptr[i] = nullptr;
+            if (a_live[i] && t >= 0 && t < sg.tin)
+                a_ptr[i] = sg.src + (((size_t)a_n[i] * sg.tin + t) * V + a_w[i]) * sg.ld + 4 * a_q[i];
+        }
+        if constexpr (PREC == PREC_F32) {
+            bcin_cur = sg.cin;
+#pragma unroll
+            for (int i = 0; i < LB; ++i)
+                b_ptr[i] = b_live[i] ? reinterpret_cast<const unsigned char*>(
+                                           sg.w + (size_t)(n0 + b_lrow[i]) * sg.ldw + tap * sg.cin + 4 * b_q[i])
+                                     : nullptr;
+        } else {
+            bcin_cur = sg.cin8;
+#pragma unroll
+            for (int i = 0; i < LB; ++i) {
+                const unsigned short* base = (b_q[i] < 4) ? sg.whi : sg.wlo;
+                b_ptr[i] = b_live[i] ? reinterpret_cast<const unsigned char*>(
+                                           base + (size_t)(n0 + b_lrow[i]) * sg.ldw8 + tap * sg.cin8 + 8 * (b_q[i] & 3))
+                                     : nullptr;
+            }
+        }
+    };
+    auto advance = [&]() {
+        c0 += BK;
+        if (c0 >= a.seg[seg].cin) {
+            c0 = 0;
+            if (++tap >= a.seg[seg].kt) { tap = 0; ++seg; }
+            if (seg < a.nseg) set_tap();
+        }
+    };
+    auto load_into = [&](f32x4 (&ra_)[LA], f32x4 (&rb_)[LB]) {
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            const int c = c0 + 4 * a_q[i];
-            const int t = sg.stride * a_t[i] + tap - sg.pad;
-            if (a_live[i] && c < sg.cin && t >= 0 && t < sg.tin) {
-                const size_t row = ((size_t)a_n[i] * sg.tin + t) * V + a_w[i];
-                v = *reinterpret_cast<const f32x4*>(sg.src + row * sg.ld + c);
-            }
-            ra[i] = v;
+            if (a_ptr[i] && c0 + 4 * a_q[i] < cin_cur) v = *reinterpret_cast<const f32x4*>(a_ptr[i] + c0);
+            ra_[i] = v;
         }
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (PREC == PREC_F32) {
-                const int c = c0 + 4 * b_q[i];
-                if (b_live[i] && c < sg.cin)
-                    v = *reinterpret_cast<const f32x4*>(sg.w + (size_t)(n0 + b_lrow[i]) * sg.ldw + tap * sg.cin + c);
-            } else {
-                const int part = b_q[i] & 3;
-                const int c = c0 + 8 * part;
-                if (b_live[i] && c < sg.cin8) {
-                    const unsigned short* base = (b_q[i] < 4) ? sg.whi : sg.wlo;
-                    v = *reinterpret_cast<const f32x4*>(base + (size_t)(n0 + b_lrow[i]) * sg.ldw8 + tap * sg.cin8 + c);
-                }
-            }
-            rb[i] = v;
+            const int cq = (PREC == PREC_F32) ? 4 * b_q[i] : 8 * (b_q[i] & 3);
+            if (b_ptr[i] && c0 + cq < bcin_cur) v = *reinterpret_cast<const f32x4*>(b_ptr[i] + c0 * PC::ESZ);
+            rb_[i] = v;
         }
     };
-    auto store_chunk = [&](int buf) {
+    f32x4 ra[LA], rb[LB], ra1[LA], rb1[LB];
+    auto store_from = [&](int buf, const f32x4 (&ra)[LA], const f32x4 (&rb)[LB]) {
         unsigned char* base = smem + buf * BUFB;
         if constexpr (PREC == PREC_F32) {
             unsigned char* As = base;
@@ -232,38 +258,37 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         }
     };
 
-    int seg = 0, tap = 0, c0 = 0;
-    auto advance = [&]() {
-        c0 += BK;
-        if (c0 >= a.seg[seg].cin) {
-            c0 = 0;
-            if (++tap >= a.seg[seg].kt) { tap = 0; ++seg; }
-        }
-    };
-
-    load_chunk(seg, tap, c0);
+    set_tap();
     if constexpr (NBUF == 2) {
-        store_chunk(0);
+        // two register sets + two LDS buffers: the global loads of chunk ch+2
+        // are issued before chunk ch computes and land in LDS after chunk ch+1
+        // computes (two compute phases of latency cover); one barrier per chunk
+        load_into(ra, rb);
+        advance();
+        if (nchunk > 1) { load_into(ra1, rb1); advance(); }
+        store_from(0, ra, rb);
         __syncthreads();
         for (int ch = 0; ch < nchunk; ++ch) {
-            const int buf = ch & 1;
-            const bool more = ch + 1 < nchunk;
-            if (more) {
+            const bool odd = ch & 1;
+            if (ch + 2 < nchunk) {
+                if (odd) load_into(ra1, rb1);
+                else load_into(ra, rb);
                 advance();
-                load_chunk(seg, tap, c0);
             }
-            compute(buf);
-            if (more) store_chunk(buf ^ 1);
+            compute(odd ? 1 : 0);
+            if (ch + 1 < nchunk) {
+                if (odd) store_from(0, ra, rb);
+                else store_from(1, ra1, rb1);
+            }
             __syncthreads();
         }
     } else {
+        load_into(ra, rb);
+        advance();
         for (int ch = 0; ch < nchunk; ++ch) {
-            store_chunk(0);
+            store_from(0, ra, rb);
             __syncthreads();
-            if (ch + 1 < nchunk) {
-                advance();
-                load_chunk(seg, tap, c0);
-            }
+            if (ch + 1 < nchunk) { load_into(ra, rb); advance(); }
             compute(0);
             __syncthreads();
         }

@@ -188,7 +188,8 @@ struct Layer {
 
     // x: rows (N*tin*V) of ld floats (>= cinp, %4); z: workspace N*tin*V*cout;
     // out: rows (N*tout*V) of cout floats.
-    int forward(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st, int prec) const {
+    int forward(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st, int prec,
+                float* part = nullptr) const {
         const int to = tout(tin, stride);
         tik::CgemmArgs g{};
         g.M = N * tin * V; g.Nc = cout; g.V = V; g.tout = tin;
@@ -225,6 +226,11 @@ struct Layer {
             const int cfg = big ? tik::CFG_T128x128 : (prec == tik::PREC_F32 ? tik::CFG_T256x64 : tik::CFG_T128x64);
             const std::string lab = std::string(big ? "T128x128.L" : (cfg == tik::CFG_T256x64 ? "T256x64.L" : "T128x64.L")) +
                                     std::to_string(index);
+            if (part) {   // small batches: split K over more workgroups (latency path)
+                t.ksplit = tik::splitk_for(t, cfg == tik::CFG_T256x64 ? 256 : 128, big ? 128 : 64,
+                                           prec == tik::PREC_F32 ? 16 : 32, 64);
+                t.partial = part;
+            }
             ProfScope p(lab.c_str(), fl, by, st);
             HIP_TRY(tik::launch_cgemm(t, cfg, st, prec));
         }
@@ -243,6 +249,7 @@ struct tik_model {
     SplitW sw0, sw3;
     int prec = 1;
     DevBuf xb, z, a0, a1, hid;     // workspace
+    DevBuf part;                   // split-K partial sums (small-batch launches)
     Profiler prof;
     bool profiling = false;
 };
@@ -327,6 +334,8 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
     md->prec = default_precision();
+    // split-K workspace: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
+    if ((rc = md->part.reserve((size_t)384 * 128 * 128))) { delete md; return rc; }
     if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
         (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
         (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
@@ -380,7 +389,7 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
     int which = 0;
     for (const Layer& L : m->layers) {
         float* o = bufs[which];
-        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st, m->prec))) return rc;
+        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st, m->prec, m->part.p))) return rc;
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);
@@ -411,6 +420,8 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
     h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = m->hid.p; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
+    h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
+    h.partial = m->part.p;
     {
         ProfScope pr("H64x64.head0", 2.0 * rows * m->feat * m->hidden,
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
@@ -420,6 +431,8 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
     p.seg[0] = mkseg(m->hid.p, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
+    p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
+    p.partial = m->part.p;
     {
         ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);

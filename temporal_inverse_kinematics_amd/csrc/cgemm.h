@@ -45,6 +45,8 @@ struct CgemmArgs {
     const float* amix;   // EPI_GRAPH: [V][V], A_eff[v][w]
     int act;
     int mix_sparse = 0;  // EPI_GRAPH: A_eff's nonzeros lie inside the COCO hop<=2 pattern
+    int ksplit = 1;      // EPI_BIAS: split K over gridDim.z workgroups (small-batch latency)
+    float* partial = nullptr;   // [ksplit][M][Nc] workspace when ksplit > 1
     // EPI_SKIN: resid = v_posed [B][ldr], out = verts [B][ldo], bias = transl [B][3] or null
 };
 
@@ -62,6 +64,9 @@ enum CgemmCfg {
 // true when every nonzero of A (V x V, row-major A[v][w]) lies in the COCO-17
 // hop<=2 pattern the sparse graph epilogue unrolls
 bool fits_coco_hop2(const float* A, int V);
+
+// split-K factor for a small launch (fewer than 128 output tiles), 1 otherwise
+int splitk_for(const CgemmArgs& a, int BM, int BN, int bk, int max_split);
 
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec = PREC_F32);
 

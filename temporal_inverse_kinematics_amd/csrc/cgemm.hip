@@ -104,8 +104,16 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         b_live[i] = (idx < NB4) && (n0 + b_lrow[i] < a.Nc);
     }
 
-    int nchunk = 0;
-    for (int s = 0; s < a.nseg; ++s) nchunk += a.seg[s].kt * ((a.seg[s].cin + BK - 1) / BK);
+    int ktotal = 0;
+    for (int s = 0; s < a.nseg; ++s) ktotal += a.seg[s].kt * ((a.seg[s].cin + BK - 1) / BK);
+    // split-K (EPI_BIAS only): workgroup z takes chunks [kbeg, kend) and writes raw partial sums
+    int kbeg = 0, nchunk = ktotal;
+    if (a.ksplit > 1) {
+        const int per = (ktotal + a.ksplit - 1) / a.ksplit;
+        kbeg = blockIdx.z * per;
+        nchunk = min(ktotal, kbeg + per) - kbeg;
+        if (nchunk < 0) nchunk = 0;
+    }
 
     // Load cursor (seg, tap, c0) and per-thread source pointers for the current
     // (seg, tap): row addresses are computed once per tap, not per chunk.
@@ -258,8 +266,21 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         }
     };
 
-    set_tap();
-    if constexpr (NBUF == 2) {
+    // position the load cursor at chunk kbeg
+    {
+        int rem = kbeg;
+        while (seg < a.nseg) {
+            const int nc = (a.seg[seg].cin + BK - 1) / BK;
+            const int segc = a.seg[seg].kt * nc;
+            if (rem < segc) { tap = rem / nc; c0 = (rem % nc) * BK; break; }
+            rem -= segc;
+            ++seg;
+        }
+    }
+    if (nchunk > 0) set_tap();
+    if (nchunk <= 0) {
+        // empty K range: contributes zeros
+    } else if constexpr (NBUF == 2) {
         // two register sets + two LDS buffers: the global loads of chunk ch+2
         // are issued before chunk ch computes and land in LDS after chunk ch+1
         // computes (two compute phases of latency cover); one barrier per chunk
@@ -311,6 +332,15 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         __syncthreads();
         constexpr int C4 = BN / 4;
         const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0);
+        if (a.ksplit > 1) {   // raw partial sums [z][M][Nc]; the reduce kernel applies the epilogue
+            float* part = a.partial + (size_t)blockIdx.z * a.M * a.Nc;
+            for (int p = tid; p < BM * BN; p += 256) {
+                const int lr = p / BN, c = p % BN;
+                const int row = r0 + lr, col = n0 + c;
+                if (row < a.M && col < a.Nc) part[(size_t)row * a.Nc + col] = Cs[lr * LDC + c];
+            }
+            return;
+        }
         for (int p = tid; p < BM * C4; p += 256) {
             const int lr = p / C4, c4 = p % C4;
             const int row = r0 + lr, col = n0 + 4 * c4;
@@ -415,9 +445,23 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     }
 }
 
+// split-K reduction + EPI_BIAS epilogue: out = act(sum_z partial[z] + bias (+ resid))
+__global__ void splitk_reduce_kernel(CgemmArgs a) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= (long long)a.M * a.Nc) return;
+    const int row = (int)(p / a.Nc), col = (int)(p % a.Nc);
+    float v = 0.f;
+    for (int z = 0; z < a.ksplit; ++z) v += a.partial[(size_t)z * a.M * a.Nc + p];
+    if (a.bias) v += a.bias[col];
+    if (a.resid) v += a.resid[(size_t)row * a.ldr + col];
+    if (a.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+    else if (a.act == ACT_LEAKY) v = v > 0.f ? v : 0.01f * v;
+    a.out[(size_t)row * a.ldo + col] = v;
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int VT>
 static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
-    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(256);
+    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN, a.ksplit > 1 ? a.ksplit : 1), blk(256);
     // the graph tile (BM=272) keeps one staging buffer in f16x3 so that two
     // workgroups fit a CU's 160 KiB of LDS
     constexpr int NB16 = (EPI == EPI_GRAPH) ? 1 : 2;
@@ -425,6 +469,12 @@ static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F16X3, NB16>), g, blk, 0, st, a);
     else
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F32, 2>), g, blk, 0, st, a);
+    if (EPI == EPI_BIAS && a.ksplit > 1) {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const long long n = (long long)a.M * a.Nc;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a);
+    }
     return hipGetLastError();
 }
 
@@ -436,8 +486,19 @@ bool fits_coco_hop2(const float* A, int V) {
     return true;
 }
 
+int splitk_for(const CgemmArgs& a, int BM, int BN, int bk, int max_split) {
+    int k = 0;
+    for (int s = 0; s < a.nseg; ++s) k += a.seg[s].kt * ((a.seg[s].cin + bk - 1) / bk);
+    const int tiles = ((a.M + BM - 1) / BM) * ((a.Nc + BN - 1) / BN);
+    if (tiles >= 128 || k < 8) return 1;
+    int s = (256 + tiles - 1) / tiles;
+    s = s > k / 2 ? k / 2 : s;
+    return s > max_split ? max_split : (s < 1 ? 1 : s);
+}
+
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
+    if (a.ksplit > 1 && !a.partial) return hipErrorInvalidValue;
     if (prec == PREC_F16X3)
         for (int s = 0; s < a.nseg; ++s)
             if (!a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;

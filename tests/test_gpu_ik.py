@@ -52,7 +52,7 @@ def test_model_ragged_vs_oracle(model, sd, N, T):
 def test_model_full_batch_consistency(model, sd):
     """Config #2 size (1024 x 64): every window equals its solo solve (batch
     independence), sampled windows match the oracle, and a checksum of the
-    per-window sums is deterministic across two launches."""
+    per-window sums is deterministic across two launches (bitwise)."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     x = syn.synthetic_windows(1024, 64, seed=0)
     xd = torch.from_numpy(x).cuda()
@@ -61,7 +61,8 @@ def test_model_full_batch_consistency(model, sd):
         y2 = model(xd)["poses"]
         solo = torch.cat([model(xd[i:i + 1])["poses"] for i in (0, 511, 1023)])
     assert torch.equal(y1, y2)
-    assert (y1[[0, 511, 1023]] - solo).abs().max().item() == 0.0
+    # a solo window takes the split-K (small-batch) path: same sums, other order
+    assert (y1[[0, 511, 1023]] - solo).abs().max().item() < 1e-5
     pick = [0, 1, 255, 700, 1023]
     ref = orc.pose_regressor(x[pick], sd)["poses"]
     assert np.abs(y1.cpu().numpy()[pick] - ref).max() < TOL

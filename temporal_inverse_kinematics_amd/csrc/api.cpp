@@ -20,6 +20,7 @@
 
 #include "../../include/tik.h"
 #include "cgemm.h"
+#include "cgemm3.h"
 #include "misc.h"
 #include "common.h"
 
@@ -56,6 +57,15 @@ int bn_fold(const TensorMap& m, const std::string& pre, int C, std::vector<float
         sh[c] = (float)((double)b->v[c] - (double)mu->v[c] * s);
     }
     return TIK_OK;
+}
+
+typedef unsigned short half_t;   // f16 bit pattern (split planes)
+
+tik::Seg3 mkseg3(const half_t* src, long long plane, const SplitW& sw, int ld, int kt, int stride, int pad, int tin) {
+    tik::Seg3 s{};
+    s.src = src; s.plane = plane; s.cin8 = sw.cin8; s.ld = ld; s.kt = kt; s.stride = stride; s.pad = pad; s.tin = tin;
+    s.whi = sw.hi.p; s.wlo = sw.lo.p; s.ldw8 = sw.ldw8;
+    return s;
 }
 
 enum ResKind { RES_ZERO = 0, RES_IDEN = 1, RES_CONV = 2 };
@@ -236,6 +246,50 @@ struct Layer {
         }
         return TIK_OK;
     }
+
+    // f16x3 on split activations (cgemm3.hip, DMA-staged). x: split planes
+    // [N*tin*V][ld] halves (lo plane xplane halves later); z / out likewise
+    // with cout halves per row and planes of rows*cout.
+    int forward3(const half_t* x, long long xplane, int ld, int N, int tin, half_t* z, half_t* out,
+                 const half_t* zeros, hipStream_t st) const {
+        const int to = tout(tin, stride);
+        const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
+        tik::Cgemm3Args g{};
+        g.M = (int)rin; g.Nc = cout; g.V = V; g.tout = tin;
+        g.seg[0] = mkseg3(x, xplane, swg, ld, 1, 1, 0, tin);
+        g.nseg = 1;
+        g.bias = bias2.p; g.out_h = z; g.out_plane = rin * cout; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
+        g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
+        const double px_in = (double)rin, px_out = (double)rout;
+        {
+            const std::string lab = "G3_272x64.L" + std::to_string(index);
+            ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                        4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+            HIP_TRY(tik::launch_cgemm3(g, tik::C3_G272x64, st));
+        }
+        tik::Cgemm3Args t{};
+        t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
+        t.seg[0] = mkseg3(z, rin * cout, swt, cout, TK, stride, 1, tin);
+        t.nseg = 1;
+        if (res == RES_CONV) {
+            t.seg[1] = mkseg3(x, xplane, swr, ld, 1, stride, 0, tin);
+            t.nseg = 2;
+        } else if (res == RES_IDEN) {
+            t.resid = x; t.resid_plane = xplane; t.ldr = ld;
+        }
+        t.bias = biasT.p; t.out_h = out; t.out_plane = rout * cout; t.ldo = cout; t.act = tik::ACT_RELU;
+        t.zeros = zeros;
+        const bool big = cout >= 128;
+        double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
+        if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
+        if (res == RES_IDEN) by += 4.0 * px_out * cout;
+        {
+            const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
+            ProfScope p(lab.c_str(), fl, by, st);
+            HIP_TRY(tik::launch_cgemm3(t, big ? tik::C3_T128x128 : tik::C3_T128x64, st));
+        }
+        return TIK_OK;
+    }
 };
 
 }  // namespace
@@ -250,6 +304,8 @@ struct tik_model {
     int prec = 1;
     DevBuf xb, z, a0, a1, hid;     // workspace
     DevBuf part;                   // split-K partial sums (small-batch launches)
+    DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
+    long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
     Profiler prof;
     bool profiling = false;
 };
@@ -268,7 +324,7 @@ struct tik_block {
 extern "C" {
 
 const char* tik_last_error(void) { return g_err.c_str(); }
-const char* tik_version(void) { return "tik 0.1.0 (gfx950, fp32 MFMA)"; }
+const char* tik_version(void) { return "tik 0.2.0 (gfx950; fp32 MFMA and f16x3 split MFMA with LDS DMA)"; }
 
 int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out) {
     if (!tensors || n_tensors <= 0 || !out) return fail(TIK_E_INVALID, "tik_model_create: null argument");
@@ -335,7 +391,14 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
     md->prec = default_precision();
     // split-K workspace: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
-    if ((rc = md->part.reserve((size_t)384 * 128 * 128))) { delete md; return rc; }
+    if ((rc = md->part.reserve((size_t)384 * 128 * 128)) || (rc = md->zeros.upload(std::vector<unsigned short>(64, 0)))) {
+        delete md;
+        return rc;
+    }
+    if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
+        if (!strcmp(e, "dma")) md->dma_min_frames = 1;
+        else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
+    }
     if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
         (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
         (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
@@ -368,15 +431,18 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
     int rc;
-    if ((rc = m->xb.reserve((size_t)N * T * V * 4)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
+    if ((rc = m->xb.reserve((size_t)N * T * V * 8)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
         (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
         return rc;
     return TIK_OK;
 }
 
+static bool use_dma(const tik_model* m, int N, int T) {
+    return m->prec == tik::PREC_F16X3 && m->dma_min_frames > 0 && (long long)N * T >= m->dma_min_frames;
+}
+
+// Backbone on fp32 activations (both precisions; split-K for small batches).
 static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st) {
-    int rc;
-    if ((rc = tik_model_reserve(m, N, T))) return rc;
     const int V = m->V;
     {
         const double px = (double)N * T * V;
@@ -384,7 +450,7 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
         HIP_TRY(tik::launch_data_bn(x, N * T * V, V, m->C0, m->bn_sc.p, m->bn_sh.p, m->xb.p, st));
     }
     const float* cur = m->xb.p;
-    int ld = 4, t = T;
+    int ld = 4, t = T, rc;
     float* bufs[2] = {m->a0.p, m->a1.p};
     int which = 0;
     for (const Layer& L : m->layers) {
@@ -397,14 +463,75 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
     return TIK_OK;
 }
 
+// Backbone on split f16 activations (f16x3, large batches): every layer reads
+// and writes hi/lo planes, operands reach LDS by DMA. Returns the hi plane of
+// the features and its plane stride.
+static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t** feat_out, long long* plane_out,
+                     int* tout, hipStream_t st) {
+    const int V = m->V;
+    half_t* xs = reinterpret_cast<half_t*>(m->xb.p);
+    const long long px = (long long)N * T * V;
+    {
+        ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
+        HIP_TRY(tik::launch_data_bn_split(x, (int)px, V, m->C0, m->bn_sc.p, m->bn_sh.p, xs, px * 8, st));
+    }
+    const half_t* cur = xs;
+    long long plane = px * 8;
+    int ld = 8, t = T, rc;
+    half_t* bufs[2] = {reinterpret_cast<half_t*>(m->a0.p), reinterpret_cast<half_t*>(m->a1.p)};
+    int which = 0;
+    for (const Layer& L : m->layers) {
+        half_t* o = bufs[which];
+        if ((rc = L.forward3(cur, plane, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st))) return rc;
+        t = Layer::tout(t, L.stride);
+        cur = o; ld = L.cout; plane = (long long)N * t * V * L.cout; which ^= 1;
+    }
+    *feat_out = cur;
+    *plane_out = plane;
+    *tout = t;
+    return TIK_OK;
+}
+
 int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream) {
     if (!m || !x || !feat || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_backbone_forward: bad arguments");
     hipStream_t st = (hipStream_t)stream;
     ProfGuard pg(m);
-    float* f;
     int to, rc;
+    if ((rc = tik_model_reserve(m, N, T))) return rc;
+    if (use_dma(m, N, T)) {
+        const half_t* f;
+        long long plane;
+        if ((rc = backbone3(m, x, N, T, &f, &plane, &to, st))) return rc;
+        HIP_TRY(tik::launch_merge(f, plane, (long long)N * to, m->feat, m->feat, feat, st));
+        return TIK_OK;
+    }
+    float* f;
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
     HIP_TRY(hipMemcpyAsync(feat, f, sizeof(float) * (size_t)N * to * m->feat, hipMemcpyDeviceToDevice, st));
+    return TIK_OK;
+}
+
+static int head3(tik_model_t m, const half_t* f, long long plane, int rows, float* poses, hipStream_t st) {
+    half_t* hs = reinterpret_cast<half_t*>(m->hid.p);
+    tik::Cgemm3Args h{};
+    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
+    h.seg[0] = mkseg3(f, plane, m->sw0, m->feat, 1, 1, 0, rows);
+    h.nseg = 1; h.bias = m->b0.p; h.out_h = hs; h.out_plane = (long long)rows * m->hidden; h.ldo = m->hidden;
+    h.act = tik::ACT_LEAKY; h.zeros = m->zeros.p;
+    {
+        ProfScope pr("H3_64x64.head0", 2.0 * rows * m->feat * m->hidden,
+                     4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
+        HIP_TRY(tik::launch_cgemm3(h, tik::C3_H64x64, st));
+    }
+    tik::Cgemm3Args p{};
+    p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
+    p.seg[0] = mkseg3(hs, (long long)rows * m->hidden, m->sw3, m->hidden, 1, 1, 0, rows);
+    p.nseg = 1; p.bias = m->b3.p; p.out_f = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE; p.zeros = m->zeros.p;
+    {
+        ProfScope pr("H3_64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
+                     4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
+        HIP_TRY(tik::launch_cgemm3(p, tik::C3_H64x64, st));
+    }
     return TIK_OK;
 }
 
@@ -414,6 +541,13 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     ProfGuard pg(m);
     float* f;
     int to, rc;
+    if ((rc = tik_model_reserve(m, N, T))) return rc;
+    if (use_dma(m, N, T)) {
+        const half_t* fs;
+        long long plane;
+        if ((rc = backbone3(m, x, N, T, &fs, &plane, &to, st))) return rc;
+        return head3(m, fs, plane, N * to, poses, st);
+    }
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
     const int rows = N * to;
     tik::CgemmArgs h{};

@@ -104,8 +104,8 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
         b_live[i] = (idx < NB4) && (n0 + b_lrow[i] < a.Nc);
     }
 
-    int ktotal = 0;
-    for (int s = 0; s < a.nseg; ++s) ktotal += a.seg[s].kt * ((a.seg[s].cin + BK - 1) / BK);
+    int ktotal = a.seg[0].kt * ((a.seg[0].cin + BK - 1) / BK);
+    if (a.nseg > 1) ktotal += a.seg[1].kt * ((a.seg[1].cin + BK - 1) / BK);
     // split-K (EPI_BIAS only): workgroup z takes chunks [kbeg, kend) and writes raw partial sums
     int kbeg = 0, nchunk = ktotal;
     if (a.ksplit > 1) {
@@ -121,8 +121,10 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     const float* a_ptr[LA];
     const unsigned char* b_ptr[LB];
     int cin_cur = 0, bcin_cur = 0;
+    // segment fields by constant index only (a runtime-indexed kernarg struct
+    // turns into vector loads + vmcnt(0) waits in the main loop)
     auto set_tap = [&]() {
-        const Seg& sg = a.seg[seg];
+        const Seg sg = (seg == 0) ? a.seg[0] : a.seg[1];
         cin_cur = sg.cin;
 #pragma unroll
         for (int i = 0; i < LA; ++i) {
@@ -149,11 +151,12 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
             }
         }
     };
+    const int cin_0 = a.seg[0].cin, cin_1 = a.seg[1].cin, kt_0 = a.seg[0].kt, kt_1 = a.seg[1].kt;
     auto advance = [&]() {
         c0 += BK;
-        if (c0 >= a.seg[seg].cin) {
+        if (c0 >= (seg == 0 ? cin_0 : cin_1)) {
             c0 = 0;
-            if (++tap >= a.seg[seg].kt) { tap = 0; ++seg; }
+            if (++tap >= (seg == 0 ? kt_0 : kt_1)) { tap = 0; ++seg; }
             if (seg < a.nseg) set_tap();
         }
     };
@@ -270,8 +273,8 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     {
         int rem = kbeg;
         while (seg < a.nseg) {
-            const int nc = (a.seg[seg].cin + BK - 1) / BK;
-            const int segc = a.seg[seg].kt * nc;
+            const int nc = ((seg == 0 ? cin_0 : cin_1) + BK - 1) / BK;
+            const int segc = (seg == 0 ? kt_0 : kt_1) * nc;
             if (rem < segc) { tap = rem / nc; c0 = (rem % nc) * BK; break; }
             rem -= segc;
             ++seg;

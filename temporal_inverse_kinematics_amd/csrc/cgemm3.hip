@@ -1,0 +1,420 @@
+// cgemm3.hip — f16x3 implicit GEMM with direct global->LDS DMA staging.
+//
+// Each stage holds, as 64-B rows (32 halves of K) with the swizzle of
+// cgemm.hip (16-B chunk c of row r at c ^ SW[(r>>2)&3]), the image
+// [A_hi | A_lo | B_hi | B_lo]. Every row chunk is one 16-B
+// global_load_lds_dwordx4: lane l of a wave-instruction writes LDS bytes
+// [16l, 16l+16) of that instruction's 1 KiB slice, so the swizzle is applied
+// on the per-lane SOURCE address (the chunk a lane fetches), never on the
+// LDS destination. Padded/out-of-range rows fetch from a zero buffer.
+//
+// Ring of NSTAGE stages; iteration ch: wait for this wave's DMAs of stage ch
+// (counted vmcnt leaves stage ch+1 in flight), s_barrier (everyone's stage ch
+// landed, everyone finished reading stage ch-1), issue stage ch+NSTAGE-1 into
+// the slot stage ch-1 used, then the MFMAs of stage ch:
+//   acc += a_lo.b_hi + a_hi.b_lo + a_hi.b_hi   (v_mfma_f32_16x16x32_f16)
+// Epilogues write split planes (or fp32 for the network's final outputs).
+#include "cgemm3.h"
+
+namespace tik {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__host__ __device__ constexpr unsigned coco_hop2_mask3(int w) {
+    constexpr unsigned m[17] = {0x1Fu,   0x3Fu,   0x5Fu,   0x8EFu,   0x1177u, 0x3BFAu, 0x5DFCu, 0xAE8u,  0x1570u,
+                                0x2A0u,  0x540u,  0xF8E8u, 0x17970u, 0xB820u, 0x15840u, 0xA800u, 0x15000u};
+    return m[w];
+}
+
+__device__ __forceinline__ int sw3(int r) { return (0x1230 >> (4 * ((r >> 2) & 3))) & 3; }
+__device__ __forceinline__ int swz3(int r, int c) { return r * 64 + ((c ^ sw3(r)) << 4); }
+
+__device__ __forceinline__ void split4(const f32x4 v, f16x4& h, f16x4& l) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        h[e] = (_Float16)v[e];
+        l[e] = (_Float16)(v[e] - (float)h[e]);
+    }
+}
+
+__device__ __forceinline__ f32x4 merge4(const unsigned short* hi, long long plane) {
+    const f16x4 h = *reinterpret_cast<const f16x4*>(hi);
+    const f16x4 l = *reinterpret_cast<const f16x4*>(hi + plane);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (float)h[e] + (float)l[e];
+    return v;
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE>
+__global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
+    constexpr int FM = BM / WM / 16;
+    constexpr int FN = BN / WN / 16;
+    static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && WM * WN == 4, "tile");
+    constexpr int R = 2 * BM + 2 * BN;          // image rows per stage
+    constexpr int NI = (R / 16 + 3) / 4;        // DMA wave-instructions per wave per stage
+    constexpr int STAGEB = NI * 4 * 1024;
+    constexpr int LDC = BN + 4;
+    constexpr int CTILE = BM * LDC * 4;
+    constexpr int SMEM = NSTAGE * STAGEB > CTILE ? NSTAGE * STAGEB : CTILE;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int r0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int V = (VT > 0) ? VT : a.V;
+
+    // ---- per-lane DMA roles: instruction j covers image rows 16*(wave*NI+j) .. +15
+    int kind[NI], ck[NI], an[NI], at[NI], aw[NI], bcol[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int r = (wave * NI + j) * 16 + (lane >> 2);
+        int rr = r, k = 4;   // 0 A_hi, 1 A_lo, 2 B_hi, 3 B_lo, 4 pad
+        if (r < BM) { k = 0; }
+        else if (r < 2 * BM) { k = 1; rr = r - BM; }
+        else if (r < 2 * BM + BN) { k = 2; rr = r - 2 * BM; }
+        else if (r < R) { k = 3; rr = r - 2 * BM - BN; }
+        ck[j] = (lane & 3) ^ sw3(rr);
+        an[j] = at[j] = aw[j] = 0;
+        bcol[j] = -1;
+        if (k <= 1) {
+            const int row = r0 + rr;
+            if (row < a.M) {
+                const int q = row / V;
+                aw[j] = row - q * V;
+                an[j] = q / a.tout;
+                at[j] = q - an[j] * a.tout;
+            } else {
+                k = 4;
+            }
+        } else if (k <= 3) {
+            bcol[j] = n0 + rr;
+            if (bcol[j] >= a.Nc) k = 4;
+        }
+        kind[j] = k;
+    }
+
+    int ktotal = a.seg[0].kt * ((a.seg[0].cin8 + 31) / 32);
+    if (a.nseg > 1) ktotal += a.seg[1].kt * ((a.seg[1].cin8 + 31) / 32);
+
+    int seg = 0, tap = 0, c0 = 0, cin8 = 0;
+    const unsigned short* base[NI];
+    // segment fields by constant index only: a runtime-indexed kernarg struct
+    // becomes vector loads + vmcnt(0) waits that would drain the DMA ring
+    auto set_tap = [&]() {
+        const Seg3 sg = (seg == 0) ? a.seg[0] : a.seg[1];
+        cin8 = sg.cin8;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const unsigned short* p = nullptr;
+            if (kind[j] <= 1) {
+                const int t = sg.stride * at[j] + tap - sg.pad;
+                if (t >= 0 && t < sg.tin)
+                    p = sg.src + (kind[j] ? sg.plane : 0) +
+                        (((long long)an[j] * sg.tin + t) * V + aw[j]) * sg.ld + 8 * ck[j];
+            } else if (kind[j] <= 3) {
+                p = (kind[j] == 2 ? sg.whi : sg.wlo) + (long long)bcol[j] * sg.ldw8 + tap * sg.cin8 + 8 * ck[j];
+            }
+            base[j] = p;
+        }
+    };
+    const int cin8_0 = a.seg[0].cin8, cin8_1 = a.seg[1].cin8, kt_0 = a.seg[0].kt, kt_1 = a.seg[1].kt;
+    auto advance = [&]() {
+        c0 += 32;
+        if (c0 >= (seg == 0 ? cin8_0 : cin8_1)) {
+            c0 = 0;
+            if (++tap >= (seg == 0 ? kt_0 : kt_1)) { tap = 0; ++seg; }
+            if (seg < a.nseg) set_tap();
+        }
+    };
+    auto issue = [&](int slot) {
+        unsigned char* dst = smem + slot * STAGEB + wave * NI * 1024;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const unsigned short* p = (base[j] && c0 + 8 * ck[j] < cin8) ? base[j] + c0 : a.zeros;
+            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int arow = wm * FM * 16 + (lane & 15);
+    const int brow = wn * FN * 16 + (lane & 15);
+    const int g = lane >> 4;
+    auto compute = [&](int slot) {
+        const unsigned char* Ahi = smem + slot * STAGEB;
+        const unsigned char* Alo = Ahi + BM * 64;
+        const unsigned char* Bhi = Alo + BM * 64;
+        const unsigned char* Blo = Bhi + BN * 64;
+        f16x8 bh[FN], bl[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int off = swz3(brow + j * 16, g);
+            bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
+            bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int off = swz3(arow + i * 16, g);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+
+    if (NSTAGE == 1 && ktotal > 0) {
+        // single stage (LDS-bound tiles): DMA of chunk ch+1 waits for compute(ch);
+        // a second resident workgroup per CU supplies the overlap
+        set_tap();
+        issue(0);
+        advance();
+        for (int ch = 0; ch < ktotal; ++ch) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            compute(0);
+            if (ch + 1 < ktotal) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                issue(0);
+                advance();
+            }
+        }
+    } else if (ktotal > 0) {
+        set_tap();
+        issue(0);
+        advance();
+#pragma unroll
+        for (int s = 1; s < NSTAGE - 1; ++s)
+            if (s < ktotal) { issue(s); advance(); }
+        for (int ch = 0; ch < ktotal; ++ch) {
+            // this wave's DMAs for stage ch are done when at most the younger
+            // stages' NI-instruction groups are still outstanding
+            const int ahead = min(NSTAGE - 2, ktotal - 1 - ch);
+            if (NSTAGE == 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (ch + NSTAGE - 1 < ktotal) {
+                issue((ch + NSTAGE - 1) % NSTAGE);
+                advance();
+            }
+            compute(ch % NSTAGE);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- epilogues (C tile staged through LDS) -----------------------------
+    const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
+    const int ccol0 = wn * FN * 16 + (lane & 15);
+    float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
+    __syncthreads();
+
+    if constexpr (EPI == EPI_BIAS) {
+        constexpr int C4 = BN / 4;
+        const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0);
+        for (int p = tid; p < BM * C4; p += 256) {
+            const int lr = p / C4, c4 = p % C4;
+            const int row = r0 + lr, col = n0 + 4 * c4;
+            if (row >= a.M || col >= a.Nc) continue;
+            const f32x4 cv = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4);
+            if (vec && col + 3 < a.Nc) {
+                f32x4 v = cv;
+                if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + col);
+                if (a.resid) v += merge4(a.resid + (size_t)row * a.ldr + col, a.resid_plane);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (a.act == ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    else if (a.act == ACT_LEAKY) v[e] = v[e] > 0.f ? v[e] : 0.01f * v[e];
+                }
+                if (a.out_h) {
+                    f16x4 h, l;
+                    split4(v, h, l);
+                    unsigned short* o = a.out_h + (size_t)row * a.ldo + col;
+                    *reinterpret_cast<f16x4*>(o) = h;
+                    *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
+                }
+                if (a.out_f) *reinterpret_cast<f32x4*>(a.out_f + (size_t)row * a.ldo + col) = v;
+            } else {
+                for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                    float v = cv[e] + (a.bias ? a.bias[col + e] : 0.f);
+                    if (a.resid) {
+                        const unsigned short* rp = a.resid + (size_t)row * a.ldr + col + e;
+                        v += (float)__builtin_bit_cast(_Float16, rp[0]) + (float)__builtin_bit_cast(_Float16, rp[a.resid_plane]);
+                    }
+                    if (a.act == ACT_RELU) v = v > 0.f ? v : 0.f;
+                    else if (a.act == ACT_LEAKY) v = v > 0.f ? v : 0.01f * v;
+                    if (a.out_h) {
+                        const _Float16 h = (_Float16)v;
+                        const _Float16 l = (_Float16)(v - (float)h);
+                        a.out_h[(size_t)row * a.ldo + col + e] = __builtin_bit_cast(unsigned short, h);
+                        a.out_h[(size_t)row * a.ldo + col + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                    }
+                    if (a.out_f) a.out_f[(size_t)row * a.ldo + col + e] = v;
+                }
+            }
+        }
+    } else {
+        // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread
+        static_assert(VT == 17 && BN % 4 == 0 && BM % VT == 0, "graph epilogue is built for the 17-joint COCO graph");
+        constexpr int FR = BM / VT;
+        constexpr int C4 = BN / 4;
+        const int frame0 = r0 / VT;
+        const int nframes = a.M / VT;
+        for (int p = tid; p < FR * C4; p += 256) {
+            const int c4 = p % C4;
+            const int f = p / C4;
+            const int col = n0 + 4 * c4;
+            if (frame0 + f >= nframes || col >= a.Nc) continue;
+            f32x4 y[VT];
+#pragma unroll
+            for (int v = 0; v < VT; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * VT + v) * LDC + 4 * c4);
+            const size_t obase = (size_t)(frame0 + f) * VT * a.ldo + col;
+            const bool full = col + 3 < a.Nc;
+#pragma unroll
+            for (int w = 0; w < VT; ++w) {
+                f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                if (a.mix_sparse) {
+#pragma unroll
+                    for (int v = 0; v < VT; ++v)
+                        if ((coco_hop2_mask3(w) >> v) & 1u) z += a.amix[v * VT + w] * y[v];
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VT; ++v) z += a.amix[v * VT + w] * y[v];
+                }
+                if (full) {
+                    z += *reinterpret_cast<const f32x4*>(a.bias + w * a.Nc + col);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                    f16x4 h, l;
+                    split4(z, h, l);
+                    unsigned short* o = a.out_h + obase + (size_t)w * a.ldo;
+                    *reinterpret_cast<f16x4*>(o) = h;
+                    *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
+                } else {
+                    for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                        float t = z[e] + a.bias[w * a.Nc + col + e];
+                        t = t > 0.f ? t : 0.f;
+                        const _Float16 h = (_Float16)t;
+                        const _Float16 l = (_Float16)(t - (float)h);
+                        a.out_h[obase + (size_t)w * a.ldo + e] = __builtin_bit_cast(unsigned short, h);
+                        a.out_h[obase + (size_t)w * a.ldo + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE>
+static hipError_t launch3(const Cgemm3Args& a, hipStream_t st) {
+    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(256);
+    hipLaunchKernelGGL((cgemm3_kernel<BM, BN, WM, WN, EPI, VT, NSTAGE>), g, blk, 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
+    if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
+    if (!a.zeros) return hipErrorInvalidValue;
+    for (int s = 0; s < a.nseg; ++s)
+        if (a.seg[s].cin8 % 8 || a.seg[s].ld % 8 || !a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    switch (cfg) {
+        case C3_T128x128: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2>(a, st);
+        case C3_T128x64: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 3>(a, st);
+        case C3_G272x64:
+            if (a.V != 17) return hipErrorInvalidValue;
+            return launch3<272, 64, 1, 4, EPI_GRAPH, 17, 1>(a, st);
+        case C3_H64x64: return launch3<64, 64, 2, 2, EPI_BIAS, 0, 3>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// ---------------------------------------------------------------- conversions
+__global__ void split_kernel(const float* __restrict__ x, long long rows, int C, int lds, int Cp,
+                             unsigned short* __restrict__ hi, long long plane) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= rows * Cp) return;
+    const long long r = p / Cp;
+    const int c = (int)(p - r * Cp);
+    const float v = c < C ? x[r * lds + c] : 0.f;
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    hi[p] = __builtin_bit_cast(unsigned short, h);
+    hi[p + plane] = __builtin_bit_cast(unsigned short, l);
+}
+
+__global__ void merge_kernel(const unsigned short* __restrict__ hi, long long plane, long long rows, int C, int ld,
+                             float* __restrict__ y) {
+    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= rows * C) return;
+    const long long r = p / C;
+    const int c = (int)(p - r * C);
+    const size_t i = (size_t)r * ld + c;
+    y[p] = (float)__builtin_bit_cast(_Float16, hi[i]) + (float)__builtin_bit_cast(_Float16, hi[i + plane]);
+}
+
+// x (px, C<=4) -> split planes (px, 8): per-(v,c) eval BN (channel v*C + c)
+__global__ void data_bn_split_kernel(const float* __restrict__ x, int n_px, int V, int C, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, unsigned short* __restrict__ hi, long long plane) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_px) return;
+    const int v = p % V;
+    f16x8 h = {}, l = {};
+    for (int c = 0; c < C && c < 8; ++c) {
+        const float t = fmaf(x[(size_t)p * C + c], scale[v * C + c], shift[v * C + c]);
+        h[c] = (_Float16)t;
+        l[c] = (_Float16)(t - (float)h[c]);
+    }
+    *reinterpret_cast<f16x8*>(hi + (size_t)p * 8) = h;
+    *reinterpret_cast<f16x8*>(hi + (size_t)p * 8 + plane) = l;
+}
+
+hipError_t launch_split(const float* x, long long rows, int C, int lds, int Cp, unsigned short* hi, long long plane,
+                        hipStream_t st) {
+    const long long n = rows * Cp;
+    if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows, C, lds, Cp, hi, plane);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const unsigned short* hi, long long plane, long long rows, int C, int ld, float* y,
+                        hipStream_t st) {
+    const long long n = rows * C;
+    if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, hi, plane, rows, C, ld, y);
+    return hipGetLastError();
+}
+
+hipError_t launch_data_bn_split(const float* x, int n_px, int V, int C, const float* scale, const float* shift,
+                                unsigned short* hi, long long plane, hipStream_t st) {
+    if (n_px <= 0) return hipSuccess;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(data_bn_split_kernel, dim3((n_px + 255) / 256), dim3(256), 0, st, x, n_px, V, C, scale, shift, hi,
+                       plane);
+    return hipGetLastError();
+}
+
+}  // namespace tik

@@ -262,10 +262,12 @@ struct Layer {
         g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
         const double px_in = (double)rin, px_out = (double)rout;
         {
-            const std::string lab = "G3_272x64.L" + std::to_string(index);
+            // 128-column tiles (8 waves) read each input row once per 128 outputs
+            const bool wide = cout % 128 == 0;
+            const std::string lab = std::string(wide ? "G3_272x128.L" : "G3_272x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
-            HIP_TRY(tik::launch_cgemm3(g, tik::C3_G272x64, st));
+            HIP_TRY(tik::launch_cgemm3(g, wide ? tik::C3_G272x128_W8 : tik::C3_G272x64, st));
         }
         tik::Cgemm3Args t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;

@@ -45,6 +45,10 @@ enum Cgemm3Cfg {
     C3_T128x64 = 1,    // tcn, C = 64
     C3_G272x64 = 2,    // gcn + graph mix (16 frames x 17 joints)
     C3_H64x64 = 3,     // head Linear layers
+    C3_T128x128_S3 = 4, C3_T128x128_S4 = 5, C3_T256x128_W8 = 6, C3_T256x64_W8 = 7, C3_T128x64_S4 = 8,
+    C3_G272x128_W8 = 9, C3_G272x64_S2 = 10,
+    C3_DBG_T128x128_DMA = 11, C3_DBG_T128x128_MFMA = 12, C3_DBG_T128x64_DMA = 13, C3_DBG_T128x64_MFMA = 14,
+    C3_NCFG = 15,
 };
 
 hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st);

@@ -48,14 +48,22 @@ __device__ __forceinline__ f32x4 merge4(const unsigned short* hi, long long plan
     return v;
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE>
-__global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// DBG (tuning only, scripts/kbench.hip): 1 = DMA without MFMA, 2 = MFMA without DMA
+template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE, int DBG = 0>
+__global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     constexpr int FM = BM / WM / 16;
     constexpr int FN = BN / WN / 16;
-    static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && WM * WN == 4, "tile");
+    constexpr int NW = WM * WN;                 // waves per workgroup
+    constexpr int NT = 64 * NW;
+    static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && (NW == 4 || NW == 8), "tile");
     constexpr int R = 2 * BM + 2 * BN;          // image rows per stage
-    constexpr int NI = (R / 16 + 3) / 4;        // DMA wave-instructions per wave per stage
-    constexpr int STAGEB = NI * 4 * 1024;
+    constexpr int NI = (R / 16 + NW - 1) / NW;  // DMA wave-instructions per wave per stage
+    constexpr int STAGEB = NI * NW * 1024;
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
     constexpr int SMEM = NSTAGE * STAGEB > CTILE ? NSTAGE * STAGEB : CTILE;
@@ -137,7 +145,7 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
             const unsigned short* p = (base[j] && c0 + 8 * ck[j] < cin8) ? base[j] + c0 : a.zeros;
-            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+            if (DBG != 2) __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
 
@@ -151,6 +159,7 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
     const int brow = wn * FN * 16 + (lane & 15);
     const int g = lane >> 4;
     auto compute = [&](int slot) {
+        if (DBG == 1) return;
         const unsigned char* Ahi = smem + slot * STAGEB;
         const unsigned char* Alo = Ahi + BM * 64;
         const unsigned char* Bhi = Alo + BM * 64;
@@ -204,8 +213,9 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
             // this wave's DMAs for stage ch are done when at most the younger
             // stages' NI-instruction groups are still outstanding
             const int ahead = min(NSTAGE - 2, ktotal - 1 - ch);
-            if (NSTAGE == 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (NSTAGE >= 4 && ahead >= 2) wait_vm<(NSTAGE >= 4 ? 2 * NI : 0)>();
+            else if (NSTAGE >= 3 && ahead >= 1) wait_vm<(NSTAGE >= 3 ? NI : 0)>();
+            else wait_vm<0>();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (ch + NSTAGE - 1 < ktotal) {
@@ -233,7 +243,7 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
     if constexpr (EPI == EPI_BIAS) {
         constexpr int C4 = BN / 4;
         const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0);
-        for (int p = tid; p < BM * C4; p += 256) {
+        for (int p = tid; p < BM * C4; p += NT) {
             const int lr = p / C4, c4 = p % C4;
             const int row = r0 + lr, col = n0 + 4 * c4;
             if (row >= a.M || col >= a.Nc) continue;
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
         constexpr int C4 = BN / 4;
         const int frame0 = r0 / VT;
         const int nframes = a.M / VT;
-        for (int p = tid; p < FR * C4; p += 256) {
+        for (int p = tid; p < FR * C4; p += NT) {
             const int c4 = p % C4;
             const int f = p / C4;
             const int col = n0 + 4 * c4;
@@ -326,10 +336,10 @@ __global__ __launch_bounds__(256) void cgemm3_kernel(Cgemm3Args a) {
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE>
+template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE, int DBG = 0>
 static hipError_t launch3(const Cgemm3Args& a, hipStream_t st) {
-    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(256);
-    hipLaunchKernelGGL((cgemm3_kernel<BM, BN, WM, WN, EPI, VT, NSTAGE>), g, blk, 0, st, a);
+    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(64 * WM * WN);
+    hipLaunchKernelGGL((cgemm3_kernel<BM, BN, WM, WN, EPI, VT, NSTAGE, DBG>), g, blk, 0, st, a);
     return hipGetLastError();
 }
 
@@ -346,6 +356,22 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
             if (a.V != 17) return hipErrorInvalidValue;
             return launch3<272, 64, 1, 4, EPI_GRAPH, 17, 1>(a, st);
         case C3_H64x64: return launch3<64, 64, 2, 2, EPI_BIAS, 0, 3>(a, st);
+        // tuning candidates (scripts/kbench.hip)
+        case C3_T128x128_S3: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 3>(a, st);
+        case C3_T128x128_S4: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 4>(a, st);
+        case C3_T256x128_W8: return launch3<256, 128, 4, 2, EPI_BIAS, 0, 3>(a, st);
+        case C3_T256x64_W8: return launch3<256, 64, 4, 2, EPI_BIAS, 0, 3>(a, st);
+        case C3_T128x64_S4: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 4>(a, st);
+        case C3_G272x128_W8:
+            if (a.V != 17) return hipErrorInvalidValue;
+            return launch3<272, 128, 1, 8, EPI_GRAPH, 17, 2>(a, st);
+        case C3_DBG_T128x128_DMA: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2, 1>(a, st);
+        case C3_DBG_T128x128_MFMA: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2, 2>(a, st);
+        case C3_DBG_T128x64_DMA: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 3, 1>(a, st);
+        case C3_DBG_T128x64_MFMA: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 3, 2>(a, st);
+        case C3_G272x64_S2:
+            if (a.V != 17) return hipErrorInvalidValue;
+            return launch3<272, 64, 1, 4, EPI_GRAPH, 17, 2>(a, st);
         default: return hipErrorInvalidValue;
     }
 }

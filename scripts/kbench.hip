@@ -70,7 +70,7 @@ static float time_launch(const tik::Cgemm3Args& a, int cfg, hipStream_t st, int 
 
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 1024, T0 = argc > 2 ? atoi(argv[2]) : 64;
-    const int reps = 20, V = 17;
+    const int reps = argc > 3 ? atoi(argv[3]) : 20, V = 17;
     struct L { int cin, cout, stride; };
     const L layers[8] = {{8, 64, 1}, {64, 64, 1}, {64, 128, 2}, {128, 128, 1},
                          {128, 128, 1}, {128, 128, 2}, {128, 256, 2}, {256, 256, 2}};

@@ -14,6 +14,8 @@
 // the slot stage ch-1 used, then the MFMAs of stage ch:
 //   acc += a_lo.b_hi + a_hi.b_lo + a_hi.b_hi   (v_mfma_f32_16x16x32_f16)
 // Epilogues write split planes (or fp32 for the network's final outputs).
+#include <type_traits>
+
 #include "cgemm3.h"
 
 namespace tik {
@@ -68,6 +70,12 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     constexpr int CTILE = BM * LDC * 4;
     constexpr int SMEM = NSTAGE * STAGEB > CTILE ? NSTAGE * STAGEB : CTILE;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+    // epilogue constants staged once, so the epilogue issues no global load
+    // behind its own stores (unknown aliasing would serialise each item)
+    constexpr int NB = (EPI == EPI_GRAPH) ? VT * BN : BN;
+    constexpr int NA = (EPI == EPI_GRAPH) ? VT * VT : 1;
+    __shared__ __attribute__((aligned(16))) float bias_s[NB];
+    __shared__ float amix_s[NA];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -106,6 +114,13 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         }
         kind[j] = k;
     }
+
+    for (int i = threadIdx.x; i < NB; i += NT) {
+        const int w = i / BN, col = n0 + i % BN;
+        bias_s[i] = (a.bias && col < a.Nc) ? a.bias[w * a.Nc + col] : 0.f;
+    }
+    if constexpr (EPI == EPI_GRAPH)
+        for (int i = threadIdx.x; i < NA; i += NT) amix_s[i] = a.amix[i];
 
     int ktotal = a.seg[0].kt * ((a.seg[0].cin8 + 31) / 32);
     if (a.nseg > 1) ktotal += a.seg[1].kt * ((a.seg[1].cin8 + 31) / 32);
@@ -242,20 +257,41 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
 
     if constexpr (EPI == EPI_BIAS) {
         constexpr int C4 = BN / 4;
-        const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0);
-        for (int p = tid; p < BM * C4; p += NT) {
-            const int lr = p / C4, c4 = p % C4;
-            const int row = r0 + lr, col = n0 + 4 * c4;
-            if (row >= a.M || col >= a.Nc) continue;
-            const f32x4 cv = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4);
-            if (vec && col + 3 < a.Nc) {
-                f32x4 v = cv;
-                if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + col);
-                if (a.resid) v += merge4(a.resid + (size_t)row * a.ldr + col, a.resid_plane);
+        static_assert(NT % C4 == 0, "epilogue mapping");
+        constexpr int RS = NT / C4;          // rows between one thread's items
+        constexpr int KI = BM / RS;          // items per thread
+        const int c4 = tid % C4, lr0 = tid / C4;
+        const int col = n0 + 4 * c4;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_s + 4 * c4);
+        const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0) && col + 3 < a.Nc;
+        if (vec) {
+            // all residual loads first, then branch-free math and the stores
+            // (a data-dependent branch between stores makes the compiler wait
+            // for every outstanding store: vmcnt counts stores too)
+            f16x4 rh[KI], rl[KI];
+#pragma unroll
+            for (int k = 0; k < KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
+            if (a.resid) {
+#pragma unroll
+                for (int k = 0; k < KI; ++k) {
+                    const int row = r0 + lr0 + k * RS;
+                    if (row < a.M) {
+                        const unsigned short* rp = a.resid + (size_t)row * a.ldr + col;
+                        rh[k] = *reinterpret_cast<const f16x4*>(rp);
+                        rl[k] = *reinterpret_cast<const f16x4*>(rp + a.resid_plane);
+                    }
+                }
+            }
+            const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
+#pragma unroll
+            for (int k = 0; k < KI; ++k) {
+                const int lr = lr0 + k * RS, row = r0 + lr;
+                if (row >= a.M) continue;
+                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4) + bv;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (a.act == ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
-                    else if (a.act == ACT_LEAKY) v[e] = v[e] > 0.f ? v[e] : 0.01f * v[e];
+                    v[e] += (float)rh[k][e] + (float)rl[k][e];
+                    v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                 }
                 if (a.out_h) {
                     f16x4 h, l;
@@ -265,9 +301,13 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                     *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
                 }
                 if (a.out_f) *reinterpret_cast<f32x4*>(a.out_f + (size_t)row * a.ldo + col) = v;
-            } else {
+            }
+        } else {
+            for (int k = 0; k < KI; ++k) {
+                const int lr = lr0 + k * RS, row = r0 + lr;
+                if (row >= a.M) continue;
                 for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
-                    float v = cv[e] + (a.bias ? a.bias[col + e] : 0.f);
+                    float v = Cs[lr * LDC + 4 * c4 + e] + bias_s[4 * c4 + e];
                     if (a.resid) {
                         const unsigned short* rp = a.resid + (size_t)row * a.ldr + col + e;
                         v += (float)__builtin_bit_cast(_Float16, rp[0]) + (float)__builtin_bit_cast(_Float16, rp[a.resid_plane]);
@@ -285,54 +325,51 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             }
         }
     } else {
-        // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread
+        // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread;
+        // A_eff and the bias come from LDS, the sparse/dense choice is hoisted
         static_assert(VT == 17 && BN % 4 == 0 && BM % VT == 0, "graph epilogue is built for the 17-joint COCO graph");
         constexpr int FR = BM / VT;
         constexpr int C4 = BN / 4;
         const int frame0 = r0 / VT;
         const int nframes = a.M / VT;
-        for (int p = tid; p < FR * C4; p += NT) {
-            const int c4 = p % C4;
-            const int f = p / C4;
-            const int col = n0 + 4 * c4;
-            if (frame0 + f >= nframes || col >= a.Nc) continue;
-            f32x4 y[VT];
+        auto mix = [&](auto sparse) {
+            for (int p = tid; p < FR * C4; p += NT) {
+                const int c4 = p % C4;
+                const int f = p / C4;
+                const int col = n0 + 4 * c4;
+                if (frame0 + f >= nframes || col >= a.Nc) continue;
+                f32x4 y[VT];
 #pragma unroll
-            for (int v = 0; v < VT; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * VT + v) * LDC + 4 * c4);
-            const size_t obase = (size_t)(frame0 + f) * VT * a.ldo + col;
-            const bool full = col + 3 < a.Nc;
+                for (int v = 0; v < VT; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * VT + v) * LDC + 4 * c4);
+                const size_t obase = (size_t)(frame0 + f) * VT * a.ldo + col;
+                const bool full = col + 3 < a.Nc;
 #pragma unroll
-            for (int w = 0; w < VT; ++w) {
-                f32x4 z = {0.f, 0.f, 0.f, 0.f};
-                if (a.mix_sparse) {
+                for (int w = 0; w < VT; ++w) {
+                    f32x4 z = *reinterpret_cast<const f32x4*>(bias_s + w * BN + 4 * c4);
 #pragma unroll
                     for (int v = 0; v < VT; ++v)
-                        if ((coco_hop2_mask3(w) >> v) & 1u) z += a.amix[v * VT + w] * y[v];
-                } else {
-#pragma unroll
-                    for (int v = 0; v < VT; ++v) z += a.amix[v * VT + w] * y[v];
-                }
-                if (full) {
-                    z += *reinterpret_cast<const f32x4*>(a.bias + w * a.Nc + col);
+                        if (!decltype(sparse)::value || ((coco_hop2_mask3(w) >> v) & 1u)) z += amix_s[v * VT + w] * y[v];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-                    f16x4 h, l;
-                    split4(z, h, l);
-                    unsigned short* o = a.out_h + obase + (size_t)w * a.ldo;
-                    *reinterpret_cast<f16x4*>(o) = h;
-                    *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
-                } else {
-                    for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
-                        float t = z[e] + a.bias[w * a.Nc + col + e];
-                        t = t > 0.f ? t : 0.f;
-                        const _Float16 h = (_Float16)t;
-                        const _Float16 l = (_Float16)(t - (float)h);
-                        a.out_h[obase + (size_t)w * a.ldo + e] = __builtin_bit_cast(unsigned short, h);
-                        a.out_h[obase + (size_t)w * a.ldo + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                    if (full) {
+                        f16x4 h, l;
+                        split4(z, h, l);
+                        unsigned short* o = a.out_h + obase + (size_t)w * a.ldo;
+                        *reinterpret_cast<f16x4*>(o) = h;
+                        *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
+                    } else {
+                        for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                            const _Float16 h = (_Float16)z[e];
+                            const _Float16 l = (_Float16)(z[e] - (float)h);
+                            a.out_h[obase + (size_t)w * a.ldo + e] = __builtin_bit_cast(unsigned short, h);
+                            a.out_h[obase + (size_t)w * a.ldo + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                        }
                     }
                 }
             }
-        }
+        };
+        if (a.mix_sparse) mix(std::true_type{});
+        else mix(std::false_type{});
     }
 }
 

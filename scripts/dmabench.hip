@@ -39,6 +39,28 @@ __global__ __launch_bounds__(256) void ldsdma_probe(const unsigned char* __restr
     if (threadIdx.x == 0 && smem[lane] == 123 && smem[1000] == 77) sink[0] = 1;
 }
 
+// fragment-shaped: each wave-instruction reads 16 rows x 64 B (4 lanes per row)
+// of rows ROWB bytes apart, i.e. half lines, like a BK=32 f16 operand tile
+template <int NI, int ROWB>
+__global__ __launch_bounds__(256) void frag_probe(const unsigned char* __restrict__ src, size_t mask, int iters, int* sink) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[32 * 1024];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // block covers 256*NI/4... rows: instruction j -> rows 16*(wave*NI+j) + lane/4, chunk lane%4
+    size_t rowbase = (size_t)blockIdx.x * 64 * NI;   // rows per block per iteration
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const size_t row = rowbase + (size_t)(wave * NI + j) * 16 + (lane >> 2);
+            dma16(src + ((row * ROWB + (lane & 3) * 16) & mask), smem + ((wave * NI + j) * 1024) % (32 * 1024));
+        }
+        rowbase += (size_t)gridDim.x * 64 * NI;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && smem[lane] == 123 && smem[1000] == 77) sink[0] = 1;
+}
+
 template <int NI>
 __global__ __launch_bounds__(256) void vgpr_probe(const unsigned char* __restrict__ src, size_t mask, int iters,
                                                   int* sink) {
@@ -80,9 +102,9 @@ int main() {
     CK(hipMemset(buf, 1, big));
     CK(hipMalloc(&sink, 4));
     const int iters = 64;
-    for (size_t span : {(size_t)1 << 21, big}) {
+    for (size_t span : {(size_t)1 << 21, (size_t)1 << 22, (size_t)1 << 23, (size_t)1 << 25, (size_t)1 << 27, (size_t)1 << 29, big}) {
         const size_t mask = span - 1;
-        for (int wg_per_cu : {1, 2, 4}) {
+        for (int wg_per_cu : {2}) {
             const int grid = 256 * wg_per_cu;
             const double bytes8 = (double)grid * 256 * 8 * 16 * iters;
             // LDS image 32 KB per workgroup (so 4 fit per CU)
@@ -92,8 +114,11 @@ int main() {
             double d8 = run([&] { hipLaunchKernelGGL(k8, dim3(grid), dim3(256), 0, 0, buf, mask, iters, sink); }, bytes8);
             double d4 = run([&] { hipLaunchKernelGGL(k4, dim3(grid), dim3(256), 0, 0, buf, mask, iters, sink); }, bytes8 / 2);
             double r8 = run([&] { hipLaunchKernelGGL(kr, dim3(grid), dim3(256), 0, 0, buf, mask, iters, sink); }, bytes8);
-            printf("span %5zu MB  wg/CU %d:  lds-dma NI=8 %6.2f TB/s  NI=4 %6.2f TB/s   reg NI=8 %6.2f TB/s\n", span >> 20,
-                   wg_per_cu, d8, d4, r8);
+            auto kf = frag_probe<8, 256>;
+            // useful bytes: 64 B per row; the rows are 256 B apart
+            double f8 = run([&] { hipLaunchKernelGGL(kf, dim3(grid), dim3(256), 0, 0, buf, mask, iters, sink); }, bytes8);
+            printf("span %5zu MB  wg/CU %d:  lds-dma NI=8 %6.2f TB/s  NI=4 %6.2f TB/s   reg NI=8 %6.2f TB/s  frag(16x64B) %6.2f TB/s\n",
+                   span >> 20, wg_per_cu, d8, d4, r8, f8);
         }
     }
     CK(hipDeviceSynchronize());

@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "cgemm3.h"
@@ -50,6 +51,30 @@ static const char* cfg_name(int c) {
                               "T256x128_W8", "T256x64_W8", "T128x64_S4", "G272x128_W8", "G272x64_S2",
                               "dbg128x128_DMA", "dbg128x128_MFMA", "dbg128x64_DMA", "dbg128x64_MFMA"};
     return c < tik::C3_NCFG ? n[c] : "?";
+}
+
+// per-workgroup phase trace (s_memrealtime, 100 MHz): main loop vs epilogue
+static void trace_launch(const char* tag, tik::Cgemm3Args a, int cfg, hipStream_t st, int nblocks) {
+    unsigned long long* d;
+    CK(hipMalloc(&d, (size_t)nblocks * 5 * 8));
+    a.trace = d;
+    for (int i = 0; i < 2; ++i) CK(tik::launch_cgemm3(a, cfg, st));
+    CK(hipStreamSynchronize(st));
+    std::vector<unsigned long long> h((size_t)nblocks * 5);
+    CK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipFree(d));
+    unsigned long long t0 = ~0ull, t2 = 0;
+    double loop = 0, epi = 0, wv = 0, wb = 0, wl = 0;
+    for (int b = 0; b < nblocks; ++b) {
+        const unsigned long long* t = &h[(size_t)b * 5];
+        t0 = std::min(t0, t[0]); t2 = std::max(t2, t[2]);
+        loop += (double)(t[1] - t[0]); epi += (double)(t[2] - t[1]);
+        wv += (double)t[3]; wb += (double)(t[4] & 0xffffffffull); wl += (double)(t[4] >> 32);
+    }
+    const double span = (double)(t2 - t0);
+    printf("  trace %-14s blocks %6d  span %8.1f us  loop %6.2f us  epilogue %6.2f us  resident/CU %.2f | wave0 loop %6.0f clk vm-wait %6.0f barrier %6.0f\n",
+           tag, nblocks, span / 100.0, loop / nblocks / 100.0, epi / nblocks / 100.0, (loop + epi) / span / 256.0,
+           wl / nblocks, wv / nblocks, wb / nblocks);
 }
 
 static float time_launch(const tik::Cgemm3Args& a, int cfg, hipStream_t st, int reps) {
@@ -99,6 +124,12 @@ int main(int argc, char** argv) {
         g.nseg = 1; g.bias = bias; g.out_h = z; g.out_plane = rin * Ly.cout; g.ldo = Ly.cout; g.amix = amix;
         g.act = 1; g.mix_sparse = 1; g.zeros = zeros;
         const int gc[] = {tik::C3_G272x64, tik::C3_G272x128_W8};
+        for (int f : {0, 1}) {
+            g.tune = f;
+            printf("L%d G %-12s %8.4f ms  flags %d\n", l, cfg_name(Ly.cout % 128 ? tik::C3_G272x64 : tik::C3_G272x128_W8),
+                   time_launch(g, Ly.cout % 128 ? tik::C3_G272x64 : tik::C3_G272x128_W8, st, reps), f);
+        }
+        g.tune = 0;
         const double gbytes = 4.0 * (rin * Ly.cin + rin * Ly.cout);
         float best = 1e9, cur = 0;
         for (int c : gc) {
@@ -121,9 +152,48 @@ int main(int argc, char** argv) {
         }
         t.bias = bias; t.out_h = o; t.out_plane = rout * Ly.cout; t.ldo = Ly.cout; t.act = 1; t.zeros = zeros;
         const double tfl = 2.0 * rout * Ly.cout * (3.0 * Ly.cout + (t.nseg > 1 ? Ly.cin : 0));
+        for (int f : {0, 1}) {
+            t.tune = f;
+            printf("L%d T %-12s %8.4f ms  flags %d\n", l, cfg_name(Ly.cout >= 128 ? tik::C3_T128x128 : tik::C3_T128x64),
+                   time_launch(t, Ly.cout >= 128 ? tik::C3_T128x128 : tik::C3_T128x64, st, reps), f);
+        }
+        t.tune = 0;
+        if (tik::tconv_halo_ok(t)) {
+            hipEvent_t e0, e1;
+            CK(hipEventCreate(&e0));
+            CK(hipEventCreate(&e1));
+            const int bn = Ly.cout >= 128 ? 128 : 64;
+            for (int i = 0; i < 3; ++i) CK(tik::launch_tconv_halo(t, bn, st));
+            CK(hipEventRecord(e0, st));
+            for (int i = 0; i < reps; ++i) CK(tik::launch_tconv_halo(t, bn, st));
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("L%d T halo%-8d %8.4f ms  %6.1f TF(fp32-eq)\n", l, bn, ms / reps,
+                   2.0 * rout * Ly.cout * (3.0 * Ly.cout + (t.nseg > 1 ? Ly.cin : 0)) / (ms / reps) / 1e9);
+            // phase trace
+            unsigned long long* d;
+            const int nb = (int)((rout + 127) / 128) * (Ly.cout / bn);
+            CK(hipMalloc(&d, (size_t)nb * 40));
+            tik::Cgemm3Args tt = t;
+            tt.trace = d;
+            CK(tik::launch_tconv_halo(tt, bn, st));
+            CK(hipStreamSynchronize(st));
+            std::vector<unsigned long long> h((size_t)nb * 5);
+            CK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+            CK(hipFree(d));
+            double lp = 0, ep = 0, wv = 0, wb = 0, wl = 0;
+            for (int b = 0; b < nb; ++b) {
+                lp += (double)(h[5 * b + 1] - h[5 * b]); ep += (double)(h[5 * b + 2] - h[5 * b + 1]);
+                wv += (double)h[5 * b + 3]; wb += (double)(h[5 * b + 4] & 0xffffffffull); wl += (double)(h[5 * b + 4] >> 32);
+            }
+            printf("  trace halo                                  loop %6.2f us  epilogue %6.2f us                  | wave0 loop %6.0f clk vm-wait %6.0f barrier %6.0f\n",
+                   lp / nb / 100.0, ep / nb / 100.0, wl / nb, wv / nb, wb / nb);
+        }
         std::vector<int> tc;
-        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T256x128_W8, tik::C3_DBG_T128x128_DMA, tik::C3_DBG_T128x128_MFMA};
-        else tc = {tik::C3_T128x64, tik::C3_T256x64_W8, tik::C3_DBG_T128x64_DMA, tik::C3_DBG_T128x64_MFMA};
+        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_DBG_T128x128_DMA, tik::C3_DBG_T128x128_MFMA};
+        else tc = {tik::C3_T128x64, tik::C3_DBG_T128x64_DMA, tik::C3_DBG_T128x64_MFMA};
         best = 1e9; cur = 0;
         for (int c : tc) {
             const float ms = time_launch(t, c, st, reps);
@@ -132,6 +202,16 @@ int main(int argc, char** argv) {
             printf("L%d T %-12s %8.4f ms  %6.1f TF(fp32-eq)\n", l, cfg_name(c), ms, tfl / ms / 1e9);
         }
         tot_best += best; tot_cur += cur;
+        {
+            const int cfgT = Ly.cout >= 128 ? tik::C3_T128x128 : tik::C3_T128x64;
+            const int nb = (int)((rout + 127) / 128) * (Ly.cout >= 128 ? (Ly.cout + 127) / 128 : (Ly.cout + 63) / 64);
+            t.tune = 0;
+            trace_launch(cfg_name(cfgT), t, cfgT, st, nb);
+            const int cfgG = Ly.cout % 128 ? tik::C3_G272x64 : tik::C3_G272x128_W8;
+            const int nbg = (int)((rin + 271) / 272) * (Ly.cout % 128 ? Ly.cout / 64 : Ly.cout / 128);
+            g.tune = 0;
+            trace_launch(cfg_name(cfgG), g, cfgG, st, nbg);
+        }
         tin = to;
     }
     printf("backbone G+T: current configs %.4f ms, best-per-launch %.4f ms\n", tot_cur, tot_best);

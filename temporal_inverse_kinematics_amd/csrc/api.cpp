@@ -251,7 +251,7 @@ struct Layer {
     // [N*tin*V][ld] halves (lo plane xplane halves later); z / out likewise
     // with cout halves per row and planes of rows*cout.
     int forward3(const half_t* x, long long xplane, int ld, int N, int tin, half_t* z, half_t* out,
-                 const half_t* zeros, hipStream_t st) const {
+                 const half_t* zeros, hipStream_t st, bool use_halo = false) const {
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         tik::Cgemm3Args g{};
@@ -285,7 +285,11 @@ struct Layer {
         double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
-        {
+        if (use_halo && tik::tconv_halo_ok(t)) {   // stride 1: taps share one LDS frame halo (tconv.hip)
+            const std::string lab = std::string(big ? "TH_128x128.L" : "TH_128x64.L") + std::to_string(index);
+            ProfScope p(lab.c_str(), fl, by, st);
+            HIP_TRY(tik::launch_tconv_halo(t, big ? 128 : 64, st));
+        } else {
             const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
             HIP_TRY(tik::launch_cgemm3(t, big ? tik::C3_T128x128 : tik::C3_T128x64, st));

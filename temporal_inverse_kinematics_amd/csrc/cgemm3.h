@@ -38,6 +38,9 @@ struct Cgemm3Args {
     int act;
     int mix_sparse;
     const unsigned short* zeros;  // >= 16 B of zeros: source of padded rows
+    int tune;                     // tuning experiments (0 = production): 1 plain tile order
+                                  // instead of the XCD-aware one
+    unsigned long long* trace;    // tuning only: per-workgroup {start, loop end, end, hw_id, xcc_id}
 };
 
 enum Cgemm3Cfg {
@@ -52,6 +55,12 @@ enum Cgemm3Cfg {
 };
 
 hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st);
+
+// stride-1 temporal conv + residual with a frame halo in LDS (tconv.hip):
+// seg[0] kt=3/stride 1/pad 1, optional seg[1] kt=1 (residual conv), V=17,
+// Nc % 64 == 0; bn = 64 or 128 output columns per tile
+bool tconv_halo_ok(const Cgemm3Args& a);
+hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st);
 
 // fp32 [rows][C] (row stride lds floats) -> split planes [rows][Cp] (zero-filled C..Cp)
 hipError_t launch_split(const float* x, long long rows, int C, int lds, int Cp, unsigned short* hi, long long plane,

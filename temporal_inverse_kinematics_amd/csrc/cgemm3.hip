@@ -16,44 +16,9 @@
 // Epilogues write split planes (or fp32 for the network's final outputs).
 #include <type_traits>
 
-#include "cgemm3.h"
+#include "cgemm3_dev.h"
 
 namespace tik {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-__host__ __device__ constexpr unsigned coco_hop2_mask3(int w) {
-    constexpr unsigned m[17] = {0x1Fu,   0x3Fu,   0x5Fu,   0x8EFu,   0x1177u, 0x3BFAu, 0x5DFCu, 0xAE8u,  0x1570u,
-                                0x2A0u,  0x540u,  0xF8E8u, 0x17970u, 0xB820u, 0x15840u, 0xA800u, 0x15000u};
-    return m[w];
-}
-
-__device__ __forceinline__ int sw3(int r) { return (0x1230 >> (4 * ((r >> 2) & 3))) & 3; }
-__device__ __forceinline__ int swz3(int r, int c) { return r * 64 + ((c ^ sw3(r)) << 4); }
-
-__device__ __forceinline__ void split4(const f32x4 v, f16x4& h, f16x4& l) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        h[e] = (_Float16)v[e];
-        l[e] = (_Float16)(v[e] - (float)h[e]);
-    }
-}
-
-__device__ __forceinline__ f32x4 merge4(const unsigned short* hi, long long plane) {
-    const f16x4 h = *reinterpret_cast<const f16x4*>(hi);
-    const f16x4 l = *reinterpret_cast<const f16x4*>(hi + plane);
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (float)h[e] + (float)l[e];
-    return v;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 // DBG (tuning only, scripts/kbench.hip): 1 = DMA without MFMA, 2 = MFMA without DMA
 template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE, int DBG = 0>
@@ -69,21 +34,36 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
     constexpr int SMEM = NSTAGE * STAGEB > CTILE ? NSTAGE * STAGEB : CTILE;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
     // epilogue constants staged once, so the epilogue issues no global load
-    // behind its own stores (unknown aliasing would serialise each item)
+    // behind its own stores (unknown aliasing would serialise each item).
+    // ALL LDS lives in one __shared__ array: a second __shared__ object beside
+    // the DMA ring makes hipcc wait vmcnt(0) before the first ds_read of every
+    // k-step, i.e. for the stage just issued, which serialises DMA and MFMA.
     constexpr int NB = (EPI == EPI_GRAPH) ? VT * BN : BN;
     constexpr int NA = (EPI == EPI_GRAPH) ? VT * VT : 1;
-    __shared__ __attribute__((aligned(16))) float bias_s[NB];
-    __shared__ float amix_s[NA];
+    constexpr int NBA = (NB + NA + 3) & ~3;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM + 4 * NBA];
+    float* bias_s = reinterpret_cast<float*>(smem + SMEM);
+    float* amix_s = bias_s + NB;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
-    const int r0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+    // (each with its own L2); give every XCD a contiguous run of tiles, column
+    // tiles of the same rows adjacent, so halo rows and column-tile re-reads
+    // hit that XCD's L2 (bijective for any grid size)
+    int r0, n0;
+    {
+        const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
+        const int swz = (a.tune & 1) ? bid : x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        r0 = (swz / gridDim.y) * BM;
+        n0 = (swz % gridDim.y) * BN;
+    }
     const int V = (VT > 0) ? VT : a.V;
+    const unsigned long long ts0 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // ---- per-lane DMA roles: instruction j covers image rows 16*(wave*NI+j) .. +15
     int kind[NI], ck[NI], an[NI], at[NI], aw[NI], bcol[NI];
@@ -155,14 +135,15 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             if (seg < a.nseg) set_tap();
         }
     };
-    auto issue = [&](int slot) {
+    auto issue_part = [&](int slot, int j0, int j1) {
         unsigned char* dst = smem + slot * STAGEB + wave * NI * 1024;
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
+        for (int j = j0; j < j1; ++j) {
             const unsigned short* p = (base[j] && c0 + 8 * ck[j] < cin8) ? base[j] + c0 : a.zeros;
             if (DBG != 2) __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
+    auto issue = [&](int slot) { issue_part(slot, 0, NI); };
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -200,7 +181,10 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         }
     };
 
-    if (NSTAGE == 1 && ktotal > 0) {
+    unsigned long long tw_vm = 0, tw_bar = 0;
+    const unsigned long long tl0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+    if constexpr (NSTAGE == 1) {
+      if (ktotal > 0) {
         // single stage (LDS-bound tiles): DMA of chunk ch+1 waits for compute(ch);
         // a second resident workgroup per CU supplies the overlap
         set_tap();
@@ -217,6 +201,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                 advance();
             }
         }
+      }
     } else if (ktotal > 0) {
         set_tap();
         issue(0);
@@ -228,11 +213,17 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             // this wave's DMAs for stage ch are done when at most the younger
             // stages' NI-instruction groups are still outstanding
             const int ahead = min(NSTAGE - 2, ktotal - 1 - ch);
+            const unsigned long long w0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
             if (NSTAGE >= 4 && ahead >= 2) wait_vm<(NSTAGE >= 4 ? 2 * NI : 0)>();
             else if (NSTAGE >= 3 && ahead >= 1) wait_vm<(NSTAGE >= 3 ? NI : 0)>();
             else wait_vm<0>();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long w1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
             __builtin_amdgcn_s_barrier();
+            if (a.trace) {
+                const unsigned long long w2 = __builtin_amdgcn_s_memtime();
+                tw_vm += w1 - w0; tw_bar += w2 - w1;
+            }
             if (ch + NSTAGE - 1 < ktotal) {
                 issue((ch + NSTAGE - 1) % NSTAGE);
                 advance();
@@ -242,6 +233,8 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const unsigned long long ts1 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long tl1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
 
     // ---- epilogues (C tile staged through LDS) -----------------------------
     const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
@@ -256,74 +249,8 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     __syncthreads();
 
     if constexpr (EPI == EPI_BIAS) {
-        constexpr int C4 = BN / 4;
-        static_assert(NT % C4 == 0, "epilogue mapping");
-        constexpr int RS = NT / C4;          // rows between one thread's items
-        constexpr int KI = BM / RS;          // items per thread
-        const int c4 = tid % C4, lr0 = tid / C4;
-        const int col = n0 + 4 * c4;
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_s + 4 * c4);
-        const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0) && col + 3 < a.Nc;
-        if (vec) {
-            // all residual loads first, then branch-free math and the stores
-            // (a data-dependent branch between stores makes the compiler wait
-            // for every outstanding store: vmcnt counts stores too)
-            f16x4 rh[KI], rl[KI];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
-            if (a.resid) {
-#pragma unroll
-                for (int k = 0; k < KI; ++k) {
-                    const int row = r0 + lr0 + k * RS;
-                    if (row < a.M) {
-                        const unsigned short* rp = a.resid + (size_t)row * a.ldr + col;
-                        rh[k] = *reinterpret_cast<const f16x4*>(rp);
-                        rl[k] = *reinterpret_cast<const f16x4*>(rp + a.resid_plane);
-                    }
-                }
-            }
-            const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const int lr = lr0 + k * RS, row = r0 + lr;
-                if (row >= a.M) continue;
-                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4) + bv;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    v[e] += (float)rh[k][e] + (float)rl[k][e];
-                    v[e] = v[e] > 0.f ? v[e] : slope * v[e];
-                }
-                if (a.out_h) {
-                    f16x4 h, l;
-                    split4(v, h, l);
-                    unsigned short* o = a.out_h + (size_t)row * a.ldo + col;
-                    *reinterpret_cast<f16x4*>(o) = h;
-                    *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
-                }
-                if (a.out_f) *reinterpret_cast<f32x4*>(a.out_f + (size_t)row * a.ldo + col) = v;
-            }
-        } else {
-            for (int k = 0; k < KI; ++k) {
-                const int lr = lr0 + k * RS, row = r0 + lr;
-                if (row >= a.M) continue;
-                for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
-                    float v = Cs[lr * LDC + 4 * c4 + e] + bias_s[4 * c4 + e];
-                    if (a.resid) {
-                        const unsigned short* rp = a.resid + (size_t)row * a.ldr + col + e;
-                        v += (float)__builtin_bit_cast(_Float16, rp[0]) + (float)__builtin_bit_cast(_Float16, rp[a.resid_plane]);
-                    }
-                    if (a.act == ACT_RELU) v = v > 0.f ? v : 0.f;
-                    else if (a.act == ACT_LEAKY) v = v > 0.f ? v : 0.01f * v;
-                    if (a.out_h) {
-                        const _Float16 h = (_Float16)v;
-                        const _Float16 l = (_Float16)(v - (float)h);
-                        a.out_h[(size_t)row * a.ldo + col + e] = __builtin_bit_cast(unsigned short, h);
-                        a.out_h[(size_t)row * a.ldo + col + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
-                    }
-                    if (a.out_f) a.out_f[(size_t)row * a.ldo + col + e] = v;
-                }
-            }
-        }
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_s + 4 * (tid % (BN / 4)));
+        epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid);
     } else {
         // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread;
         // A_eff and the bias come from LDS, the sparse/dense choice is hoisted
@@ -370,6 +297,16 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         };
         if (a.mix_sparse) mix(std::true_type{});
         else mix(std::false_type{});
+    }
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long* t = a.trace + 5 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+            t[0] = ts0; t[1] = ts1; t[2] = __builtin_amdgcn_s_memrealtime();
+            t[3] = tw_vm;    // wave 0: cycles in the DMA wait
+            t[4] = tw_bar | ((unsigned long long)(tl1 - tl0) << 32);   // barrier cycles | loop cycles << 32
+        }
     }
 }
 

@@ -1,0 +1,249 @@
+// tconv.hip — the stride-1 temporal conv (tcn.2, kernel 3, pad 1) of an
+// ST-GCN block with its residual, on split f16 activations, with a frame
+// HALO instead of three shifted operand copies.
+//
+// A 128-row output tile covers at most 9 frames of the 17-joint graph; its
+// three temporal taps read input frames q-1, q, q+1, i.e. at most 11 frames
+// (187 rows). cgemm3 streams those rows three times (once per tap); here each
+// 32-channel chunk of the halo is DMA'd into LDS once and the three taps read
+// it at row offsets -17, 0, +17. Taps that fall outside the sample's window
+// (zero padding of the reference conv, st_gcn_aaai18.py tcn) read a zero row
+// of the halo image. The residual conv (1x1, same frames) reuses the halo
+// machinery with the centre tap only. Epilogue as cgemm3 (bias, residual,
+// ReLU, split store).
+//
+// Pipeline (one chunk in flight, two blocks per CU): iteration it = (group g
+// = channel chunk of a segment, tap k). Per iteration the B tile (weights of
+// tap k for this chunk) is DMA'd into a 2-deep ring; per group the halo is
+// DMA'd into a 2-deep ring one iteration ahead of its first use.
+#include "cgemm3_dev.h"
+
+namespace tik {
+
+template <int BN>
+__global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
+    constexpr int BM = 128, WM = 2, WN = 2, NT = 256;
+    constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+    constexpr int HMAX = 192;             // halo rows in the image (>= 11 frames x 17)
+    constexpr int ZR = HMAX - 1;          // a row that is always zero-filled
+    constexpr int ASLOT = 2 * HMAX * 64;  // hi + lo planes, 64-B rows
+    constexpr int BSLOT = 2 * BN * 64;
+    constexpr int NIA = 2 * HMAX / 16 / 4;   // halo DMA wave-instructions per wave
+    constexpr int NIB = 2 * BN / 16 / 4;     // weight DMA wave-instructions per wave
+    constexpr int LDC = BN + 4;
+    constexpr int CTILE = BM * LDC * 4;
+    constexpr int RING = 2 * ASLOT + 2 * BSLOT;
+    constexpr int SMEM = RING > CTILE ? RING : CTILE;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int V = a.V, M = a.M, tin = a.tout;
+    int r0, n0;
+    {   // XCD-aware tile order (cgemm3.hip)
+        const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
+        const int swz = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        r0 = (swz / gridDim.y) * BM;
+        n0 = (swz % gridDim.y) * BN;
+    }
+    const unsigned long long ts0 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // halo frames [F0, F0 + HR/V) of the flattened (sample, frame) axis
+    const int Q = M / V;
+    const int q0 = r0 / V, q1 = (min(r0 + BM, M) - 1) / V;
+    const int F0 = max(q0 - 1, 0), F1 = min(q1 + 1, Q - 1);
+    const int HR = (F1 - F0 + 1) * V;
+
+    // per-lane A-fragment halo rows: centre-tap row hr1[i]; taps 0 / 2 are
+    // hr1 -/+ V when that frame lies inside the sample (bit 2i / 2i+1 of
+    // tapok), else the zero row. Kept as scalars per fragment and combined
+    // arithmetically each iteration: an indexed [tap][i] table is lowered to
+    // scratch memory, whose loads would queue behind the in-flight DMAs.
+    const int g = lane >> 4;
+    int hr1[FM];
+    unsigned tapok = 0;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int r = r0 + wm * FM * 16 + i * 16 + (lane & 15);
+        const int q = r / V, w = r - q * V, t = q % tin;
+        hr1[i] = r < M ? (q - F0) * V + w : ZR;
+        if (r < M && t >= 1) tapok |= 1u << (2 * i);
+        if (r < M && t + 1 < tin) tapok |= 2u << (2 * i);
+    }
+
+    // DMA roles. Halo instruction j: image row ir -> plane ir / HMAX, halo row ir % HMAX.
+    int a_row[NIA], a_ck[NIA], a_pl[NIA];
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+        const int ir = (wave * NIA + j) * 16 + (lane >> 2);
+        const int hrow = ir % HMAX;
+        a_pl[j] = ir / HMAX;
+        a_ck[j] = (lane & 3) ^ sw3(hrow);
+        a_row[j] = hrow < HR ? F0 * V + hrow : -1;
+    }
+    int b_col[NIB], b_ck[NIB], b_pl[NIB];
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+        const int ir = (wave * NIB + j) * 16 + (lane >> 2);
+        const int rr = ir % BN;
+        b_pl[j] = ir / BN;
+        b_ck[j] = (lane & 3) ^ sw3(rr);
+        b_col[j] = n0 + rr < a.Nc ? n0 + rr : -1;
+    }
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    {
+        const int col = n0 + 4 * (tid % (BN / 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (a.bias && col + e < a.Nc) bv[e] = a.bias[col + e];
+    }
+
+    // iteration space: segment 0 (taps 0,1,2 per chunk), segment 1 (centre tap)
+    const int G0 = (a.seg[0].cin8 + 31) / 32;
+    const int G1 = a.nseg > 1 ? (a.seg[1].cin8 + 31) / 32 : 0;
+    const int NIT = 3 * G0 + G1;
+
+    auto issue_halo = [&](int grp, int slot, int j0, int j1) {
+        const bool s1 = grp >= G0;
+        const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
+        const int c0 = 32 * (s1 ? grp - G0 : grp);
+        unsigned char* dst = smem + slot * ASLOT + wave * NIA * 1024;
+#pragma unroll
+        for (int j = j0; j < j1; ++j) {
+            const unsigned short* p = a.zeros;
+            if (a_row[j] >= 0 && c0 + 8 * a_ck[j] < sg.cin8)
+                p = sg.src + (a_pl[j] ? sg.plane : 0) + (long long)a_row[j] * sg.ld + c0 + 8 * a_ck[j];
+            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+        }
+    };
+    auto issue_w = [&](int grp, int tap, int slot, int j0, int j1) {
+        const bool s1 = grp >= G0;
+        const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
+        const int c0 = 32 * (s1 ? grp - G0 : grp);
+        unsigned char* dst = smem + 2 * ASLOT + slot * BSLOT + wave * NIB * 1024;
+#pragma unroll
+        for (int j = j0; j < j1; ++j) {
+            const unsigned short* p = a.zeros;
+            if (b_col[j] >= 0 && c0 + 8 * b_ck[j] < sg.cin8)
+                p = (b_pl[j] ? sg.wlo : sg.whi) + (long long)b_col[j] * sg.ldw8 + (s1 ? 0 : tap) * sg.cin8 + c0 + 8 * b_ck[j];
+            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int brow = wn * FN * 16 + (lane & 15);
+    // MFMAs of one iteration, with the next iteration's DMAs (gn >= 0: weight
+    // tile of group gn / tap tn; hnew: also the halo of group gn) spread
+    // between the fragment groups
+    auto compute = [&](int aslot, int bslot, int tap, int gn, int tn, bool hnew) {
+        const unsigned char* Ahi = smem + aslot * ASLOT;
+        const unsigned char* Alo = Ahi + HMAX * 64;
+        const unsigned char* Bhi = smem + 2 * ASLOT + bslot * BSLOT;
+        const unsigned char* Blo = Bhi + BN * 64;
+        f16x8 bh[FN], bl[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int off = swz3(brow + j * 16, g);
+            bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
+            bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            int hr = hr1[i];
+            if (tap != 1) hr = ((tapok >> (2 * i + (tap >> 1))) & 1u) ? hr + (tap - 1) * V : ZR;
+            const int off = swz3(hr, g);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+            }
+            if (gn >= 0) {
+                issue_w(gn, tn, bslot ^ 1, (i * NIB) / FM, ((i + 1) * NIB) / FM);
+                if (hnew) issue_halo(gn, gn & 1, (i * NIA) / FM, ((i + 1) * NIA) / FM);
+            }
+        }
+    };
+
+    // (group, tap) of iteration it: groups < G0 have 3 taps, the rest 1 (centre)
+    auto it_group = [&](int it) { return it < 3 * G0 ? it / 3 : G0 + (it - 3 * G0); };
+    auto it_tap = [&](int it) { return it < 3 * G0 ? it % 3 : 1; };
+    unsigned long long tw_vm = 0, tw_bar = 0;
+    const unsigned long long tl0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+    if (NIT > 0) {
+        issue_halo(0, 0, 0, NIA);
+        issue_w(0, it_tap(0), 0, 0, NIB);
+        for (int it = 0; it < NIT; ++it) {
+            const unsigned long long w0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long w1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+            __builtin_amdgcn_s_barrier();
+            if (a.trace) {
+                const unsigned long long w2 = __builtin_amdgcn_s_memtime();
+                tw_vm += w1 - w0; tw_bar += w2 - w1;
+            }
+            const int grp = it_group(it);
+            const int gn = it + 1 < NIT ? it_group(it + 1) : -1;
+            compute(grp & 1, it & 1, it_tap(it), gn, it + 1 < NIT ? it_tap(it + 1) : 0, gn >= 0 && gn != grp);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long ts1 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long tl1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+
+    const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
+    const int ccol0 = wn * FN * 16 + (lane & 15);
+    float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
+    __syncthreads();
+    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid);
+
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long* t = a.trace + 5 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+            t[0] = ts0; t[1] = ts1; t[2] = __builtin_amdgcn_s_memrealtime();
+            t[3] = tw_vm;    // wave 0: cycles in the DMA wait
+            t[4] = tw_bar | ((unsigned long long)(tl1 - tl0) << 32);   // barrier cycles | loop cycles << 32
+        }
+    }
+}
+
+bool tconv_halo_ok(const Cgemm3Args& a) {
+    const Seg3& s0 = a.seg[0];
+    if (a.V != 17 || a.M % a.V || s0.kt != 3 || s0.stride != 1 || s0.pad != 1 || s0.tin != a.tout) return false;
+    if (a.nseg > 1) {
+        const Seg3& s1 = a.seg[1];
+        if (s1.kt != 1 || s1.stride != 1 || s1.pad != 0 || s1.tin != a.tout) return false;
+    }
+    return a.zeros && (a.Nc % 64 == 0);
+}
+
+hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st) {
+    if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
+    if (!tconv_halo_ok(a) || (bn != 64 && bn != 128)) return hipErrorInvalidValue;
+    for (int s = 0; s < a.nseg; ++s)
+        if (a.seg[s].cin8 % 8 || a.seg[s].ld % 8 || !a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    const dim3 grid((a.M + 127) / 128, (a.Nc + bn - 1) / bn), blk(256);
+    if (bn == 128) hipLaunchKernelGGL(tconv_halo_kernel<128>, grid, blk, 0, st, a);
+    else hipLaunchKernelGGL(tconv_halo_kernel<64>, grid, blk, 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace tik

@@ -97,16 +97,15 @@ int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 1024, T0 = argc > 2 ? atoi(argv[2]) : 64;
     const int reps = argc > 3 ? atoi(argv[3]) : 20, V = 17;
     struct L { int cin, cout, stride; };
-    const L layers[8] = {{8, 64, 1}, {64, 64, 1}, {64, 128, 2}, {128, 128, 1},
+    const L layers[8] = {{4, 64, 1}, {64, 64, 1}, {64, 128, 2}, {128, 128, 1},
                          {128, 128, 1}, {128, 128, 2}, {128, 256, 2}, {256, 256, 2}};
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const size_t maxrows = (size_t)N * T0 * V;
-    half_t* x = dev_halves(maxrows * 256 * 2, 1);
+    half_t* x = dev_halves(maxrows * 256 * 2, 1);   // SB rows (layer 0: one 32-channel block)
     half_t* z = dev_halves(maxrows * 256 * 2, 2);
     half_t* o = dev_halves(maxrows * 256 * 2, 3);
-    half_t* wh = dev_halves(256 * 3 * 256, 4);
-    half_t* wl = dev_halves(256 * 3 * 256, 5);
+    half_t* wsb = dev_halves(256 * 3 * 8 * 64, 4);   // SB weights, up to Nc=256, kt=3, 8 blocks
     half_t* zeros;
     CK(hipMalloc(&zeros, 256));
     CK(hipMemset(zeros, 0, 256));
@@ -120,8 +119,9 @@ int main(int argc, char** argv) {
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         tik::Cgemm3Args g{};
         g.M = (int)rin; g.Nc = Ly.cout; g.V = V; g.tout = tin;
-        g.seg[0] = tik::Seg3{x, rin * Ly.cin, Ly.cin, Ly.cin, 1, 1, 0, tin, wh, wl, Ly.cin};
-        g.nseg = 1; g.bias = bias; g.out_h = z; g.out_plane = rin * Ly.cout; g.ldo = Ly.cout; g.amix = amix;
+        const int nbi = tik::sb_blocks(Ly.cin), nbo = tik::sb_blocks(Ly.cout);
+        g.seg[0] = tik::Seg3{x, nbi, 64 * nbi, 1, 1, 0, tin, wsb, 64 * nbi};
+        g.nseg = 1; g.bias = bias; g.out_h = z; g.ldo = 64 * nbo; g.amix = amix;
         g.act = 1; g.mix_sparse = 1; g.zeros = zeros;
         const int gc[] = {tik::C3_G272x64, tik::C3_G272x128_W8};
         for (int f : {0, 1}) {
@@ -142,15 +142,15 @@ int main(int argc, char** argv) {
         tot_best += best; tot_cur += cur;
         tik::Cgemm3Args t{};
         t.M = (int)rout; t.Nc = Ly.cout; t.V = V; t.tout = to;
-        t.seg[0] = tik::Seg3{z, rin * Ly.cout, Ly.cout, Ly.cout, 3, Ly.stride, 1, tin, wh, wl, 3 * Ly.cout};
+        t.seg[0] = tik::Seg3{z, nbo, 64 * nbo, 3, Ly.stride, 1, tin, wsb, 3 * 64 * nbo};
         t.nseg = 1;
         if (Ly.cin != Ly.cout || Ly.stride != 1) {
-            t.seg[1] = tik::Seg3{x, rin * Ly.cin, Ly.cin, Ly.cin, 1, Ly.stride, 0, tin, wh, wl, Ly.cin};
+            t.seg[1] = tik::Seg3{x, nbi, 64 * nbi, 1, Ly.stride, 0, tin, wsb, 64 * nbi};
             t.nseg = 2;
         } else {
-            t.resid = x; t.resid_plane = rin * Ly.cin; t.ldr = Ly.cin;
+            t.resid = x; t.ldr = 64 * nbi;
         }
-        t.bias = bias; t.out_h = o; t.out_plane = rout * Ly.cout; t.ldo = Ly.cout; t.act = 1; t.zeros = zeros;
+        t.bias = bias; t.out_h = o; t.ldo = 64 * nbo; t.act = 1; t.zeros = zeros;
         const double tfl = 2.0 * rout * Ly.cout * (3.0 * Ly.cout + (t.nseg > 1 ? Ly.cin : 0));
         for (int f : {0, 1}) {
             t.tune = f;
@@ -192,8 +192,8 @@ int main(int argc, char** argv) {
                    lp / nb / 100.0, ep / nb / 100.0, wl / nb, wv / nb, wb / nb);
         }
         std::vector<int> tc;
-        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_DBG_T128x128_DMA, tik::C3_DBG_T128x128_MFMA};
-        else tc = {tik::C3_T128x64, tik::C3_DBG_T128x64_DMA, tik::C3_DBG_T128x64_MFMA};
+        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T256x128_W8, tik::C3_T128x128_S3, tik::C3_T128x64};
+        else tc = {tik::C3_T128x64, tik::C3_T256x64_W8, tik::C3_T128x64_S4};
         best = 1e9; cur = 0;
         for (int c : tc) {
             const float ms = time_launch(t, c, st, reps);

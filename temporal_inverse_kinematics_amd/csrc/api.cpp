@@ -59,12 +59,12 @@ int bn_fold(const TensorMap& m, const std::string& pre, int C, std::vector<float
     return TIK_OK;
 }
 
-typedef unsigned short half_t;   // f16 bit pattern (split planes)
+typedef unsigned short half_t;   // f16 bit pattern (split-block activations)
 
-tik::Seg3 mkseg3(const half_t* src, long long plane, const SplitW& sw, int ld, int kt, int stride, int pad, int tin) {
+tik::Seg3 mkseg3(const half_t* src, int ld, const SBW& w, int kt, int stride, int pad, int tin) {
     tik::Seg3 s{};
-    s.src = src; s.plane = plane; s.cin8 = sw.cin8; s.ld = ld; s.kt = kt; s.stride = stride; s.pad = pad; s.tin = tin;
-    s.whi = sw.hi.p; s.wlo = sw.lo.p; s.ldw8 = sw.ldw8;
+    s.src = src; s.nblk = w.nblk; s.ld = ld; s.kt = kt; s.stride = stride; s.pad = pad; s.tin = tin;
+    s.w = w.w.p; s.ldw = w.ldw;
     return s;
 }
 
@@ -129,7 +129,8 @@ struct Layer {
     DevBuf wt;      // [cout][3*cout]        tcn conv scaled by tcn.3 BN, k = tap*cout + ci
     DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
-    SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3)
+    SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3, register-staged path)
+    SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -183,13 +184,15 @@ struct Layer {
                 for (int ci = 0; ci < cin; ++ci) hwr[(size_t)co * cinp + ci] = scr[co] * Wr->v[(size_t)co * cin + ci];
                 hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
             }
-            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp))) return rc;
+            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)))
+                return rc;
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
         mix_sparse = tik::fits_coco_hop2(ha.data(), V);
         if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
             (rc = biasT.upload(hbt)) || (rc = swg.build(hwg, cout, 1, cinp, cinp)) ||
-            (rc = swt.build(hwt, cout, TK, cout, TK * cout)))
+            (rc = swt.build(hwt, cout, TK, cout, TK * cout)) || (rc = sbg.build(hwg, cout, 1, cinp, cinp)) ||
+            (rc = sbt.build(hwt, cout, TK, cout, TK * cout)))
             return rc;
         return TIK_OK;
     }
@@ -247,18 +250,18 @@ struct Layer {
         return TIK_OK;
     }
 
-    // f16x3 on split activations (cgemm3.hip, DMA-staged). x: split planes
-    // [N*tin*V][ld] halves (lo plane xplane halves later); z / out likewise
-    // with cout halves per row and planes of rows*cout.
-    int forward3(const half_t* x, long long xplane, int ld, int N, int tin, half_t* z, half_t* out,
-                 const half_t* zeros, hipStream_t st, bool use_halo = false) const {
+    // f16x3 on split-block activations (cgemm3.hip, DMA-staged). x: SB rows
+    // [N*tin*V][ld] halves; z / out: SB rows of 64*ceil(cout/32) halves.
+    int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
+                 bool use_halo = true) const {
+        const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         tik::Cgemm3Args g{};
         g.M = (int)rin; g.Nc = cout; g.V = V; g.tout = tin;
-        g.seg[0] = mkseg3(x, xplane, swg, ld, 1, 1, 0, tin);
+        g.seg[0] = mkseg3(x, ld, sbg, 1, 1, 0, tin);
         g.nseg = 1;
-        g.bias = bias2.p; g.out_h = z; g.out_plane = rin * cout; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
+        g.bias = bias2.p; g.out_h = z; g.ldo = ldz; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
         const double px_in = (double)rin, px_out = (double)rout;
         {
@@ -271,15 +274,15 @@ struct Layer {
         }
         tik::Cgemm3Args t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
-        t.seg[0] = mkseg3(z, rin * cout, swt, cout, TK, stride, 1, tin);
+        t.seg[0] = mkseg3(z, ldz, sbt, TK, stride, 1, tin);
         t.nseg = 1;
         if (res == RES_CONV) {
-            t.seg[1] = mkseg3(x, xplane, swr, ld, 1, stride, 0, tin);
+            t.seg[1] = mkseg3(x, ld, sbr, 1, stride, 0, tin);
             t.nseg = 2;
         } else if (res == RES_IDEN) {
-            t.resid = x; t.resid_plane = xplane; t.ldr = ld;
+            t.resid = x; t.ldr = ld;
         }
-        t.bias = biasT.p; t.out_h = out; t.out_plane = rout * cout; t.ldo = cout; t.act = tik::ACT_RELU;
+        t.bias = biasT.p; t.out_h = out; t.ldo = ldz; t.act = tik::ACT_RELU;
         t.zeros = zeros;
         const bool big = cout >= 128;
         double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
@@ -307,6 +310,7 @@ struct tik_model {
     DevBuf bn_sc, bn_sh;           // data_bn (V*C0)
     DevBuf w0, b0, w3, b3;         // head
     SplitW sw0, sw3;
+    SBW sb0, sb3;
     int prec = 1;
     DevBuf xb, z, a0, a1, hid;     // workspace
     DevBuf part;                   // split-K partial sums (small-batch launches)
@@ -407,7 +411,9 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     }
     if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
         (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
-        (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
+        (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
+        (rc = md->sb0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
+        (rc = md->sb3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
         delete md;
         return rc;
     }
@@ -437,7 +443,7 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
     int rc;
-    if ((rc = m->xb.reserve((size_t)N * T * V * 8)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
+    if ((rc = m->xb.reserve((size_t)N * T * V * 32)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
         (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
         return rc;
     return TIK_OK;
@@ -469,31 +475,30 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
     return TIK_OK;
 }
 
-// Backbone on split f16 activations (f16x3, large batches): every layer reads
-// and writes hi/lo planes, operands reach LDS by DMA. Returns the hi plane of
-// the features and its plane stride.
-static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t** feat_out, long long* plane_out,
-                     int* tout, hipStream_t st) {
+// Backbone on split-block f16 activations (f16x3, large batches): every
+// layer reads and writes SB rows, operands reach LDS by DMA. Returns the
+// features (SB rows of the last layer) and their row stride.
+static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t** feat_out, int* ld_out, int* tout,
+                     hipStream_t st) {
     const int V = m->V;
     half_t* xs = reinterpret_cast<half_t*>(m->xb.p);
     const long long px = (long long)N * T * V;
     {
         ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
-        HIP_TRY(tik::launch_data_bn_split(x, (int)px, V, m->C0, m->bn_sc.p, m->bn_sh.p, xs, px * 8, st));
+        HIP_TRY(tik::launch_data_bn_split(x, (int)px, V, m->C0, m->bn_sc.p, m->bn_sh.p, xs, st));
     }
     const half_t* cur = xs;
-    long long plane = px * 8;
-    int ld = 8, t = T, rc;
+    int ld = 64, t = T, rc;
     half_t* bufs[2] = {reinterpret_cast<half_t*>(m->a0.p), reinterpret_cast<half_t*>(m->a1.p)};
     int which = 0;
     for (const Layer& L : m->layers) {
         half_t* o = bufs[which];
-        if ((rc = L.forward3(cur, plane, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st))) return rc;
+        if ((rc = L.forward3(cur, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st))) return rc;
         t = Layer::tout(t, L.stride);
-        cur = o; ld = L.cout; plane = (long long)N * t * V * L.cout; which ^= 1;
+        cur = o; ld = 64 * L.sbt.nblk; which ^= 1;
     }
     *feat_out = cur;
-    *plane_out = plane;
+    *ld_out = ld;
     *tout = t;
     return TIK_OK;
 }
@@ -506,9 +511,10 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     if ((rc = tik_model_reserve(m, N, T))) return rc;
     if (use_dma(m, N, T)) {
         const half_t* f;
-        long long plane;
-        if ((rc = backbone3(m, x, N, T, &f, &plane, &to, st))) return rc;
-        HIP_TRY(tik::launch_merge(f, plane, (long long)N * to, m->feat, m->feat, feat, st));
+        int ld;
+        if ((rc = backbone3(m, x, N, T, &f, &ld, &to, st))) return rc;
+        const int C = m->layers.back().cout;
+        HIP_TRY(tik::launch_merge(f, (long long)N * to * m->V, C, ld, feat, st));
         return TIK_OK;
     }
     float* f;
@@ -517,12 +523,16 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     return TIK_OK;
 }
 
-static int head3(tik_model_t m, const half_t* f, long long plane, int rows, float* poses, hipStream_t st) {
+static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses, hipStream_t st) {
+    // the features of one frame are its V joint rows back to back: one SB row
+    // of V * ldf halves whose blocks run over (joint, channel) = the reference
+    // flatten order (st_gcn_aaai18.py:131-132)
     half_t* hs = reinterpret_cast<half_t*>(m->hid.p);
+    const int ldh = 64 * m->sb3.nblk;
     tik::Cgemm3Args h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = mkseg3(f, plane, m->sw0, m->feat, 1, 1, 0, rows);
-    h.nseg = 1; h.bias = m->b0.p; h.out_h = hs; h.out_plane = (long long)rows * m->hidden; h.ldo = m->hidden;
+    h.seg[0] = mkseg3(f, m->V * ldf, m->sb0, 1, 1, 0, rows);
+    h.nseg = 1; h.bias = m->b0.p; h.out_h = hs; h.ldo = ldh;
     h.act = tik::ACT_LEAKY; h.zeros = m->zeros.p;
     {
         ProfScope pr("H3_64x64.head0", 2.0 * rows * m->feat * m->hidden,
@@ -531,8 +541,8 @@ static int head3(tik_model_t m, const half_t* f, long long plane, int rows, floa
     }
     tik::Cgemm3Args p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = mkseg3(hs, (long long)rows * m->hidden, m->sw3, m->hidden, 1, 1, 0, rows);
-    p.nseg = 1; p.bias = m->b3.p; p.out_f = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE; p.zeros = m->zeros.p;
+    p.seg[0] = mkseg3(hs, ldh, m->sb3, 1, 1, 0, rows);
+    p.nseg = 1; p.bias = m->b3.p; p.out_f = poses; p.ldf = m->pose_dim; p.act = tik::ACT_NONE; p.zeros = m->zeros.p;
     {
         ProfScope pr("H3_64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
@@ -550,9 +560,9 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     if ((rc = tik_model_reserve(m, N, T))) return rc;
     if (use_dma(m, N, T)) {
         const half_t* fs;
-        long long plane;
-        if ((rc = backbone3(m, x, N, T, &fs, &plane, &to, st))) return rc;
-        return head3(m, fs, plane, N * to, poses, st);
+        int ld;
+        if ((rc = backbone3(m, x, N, T, &fs, &ld, &to, st))) return rc;
+        return head3(m, fs, ld, N * to, poses, st);
     }
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
     const int rows = N * to;

@@ -1,11 +1,14 @@
-// cgemm3.h — the f16x3 implicit-GEMM path on split activations.
+// cgemm3.h — the f16x3 implicit-GEMM path on split-block activations.
 //
 // Same contraction as cgemm.h (rows r = (n*tout + t')*V + w, temporal taps,
-// up to two K segments), but every operand is stored pre-split as two f16
-// planes (hi = f16(x), lo = f16(x - hi)): activations [rows][ld] halves with
-// the lo plane `plane` halves after the hi plane; weights [Nc][kt*cin8].
-// Operands reach LDS by direct global->LDS DMA (global_load_lds_dwordx4) in a
-// 3-stage ring: no VGPR staging, no conversion VALU, two chunks of prefetch.
+// up to two K segments), but every operand is stored pre-split in the
+// SPLIT-BLOCK ("SB") layout: channels in blocks of 32, each block 64 halves =
+// [hi(x) for its 32 channels | lo(x) = f16(x - hi) for the same 32], i.e. one
+// full 128-B line per row per block. Channel c of row r:
+//     hi at r*ld + (c/32)*64 + c%32,   lo at that + 32.
+// Weights use the same blocks along K: [Nc][tap][block][64]. Operands reach
+// LDS by direct global->LDS DMA (global_load_lds_dwordx4), each wave
+// instruction moving 8 full rows x 128 B.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -14,12 +17,12 @@
 namespace tik {
 
 struct Seg3 {
-    const unsigned short* src;   // hi plane; lo plane at src + plane
-    long long plane;
-    int cin8, ld, kt, stride, pad, tin;   // cin8 % 8 == 0, ld % 8 == 0 (halves)
-    const unsigned short* whi;   // [Nc][ldw8] weights, k = tap*cin8 + ci
-    const unsigned short* wlo;
-    int ldw8;
+    const unsigned short* src;   // SB activations [rows][ld]
+    int nblk;                    // 32-channel blocks per tap (K = kt * nblk * 32)
+    int ld;                      // halves per activation row (>= 64 * nblk)
+    int kt, stride, pad, tin;
+    const unsigned short* w;     // SB weights [Nc][ldw], ldw = kt * nblk * 64
+    int ldw;
 };
 
 struct Cgemm3Args {
@@ -27,20 +30,19 @@ struct Cgemm3Args {
     Seg3 seg[2];
     int nseg;
     const float* bias;            // EPI_BIAS [Nc]; EPI_GRAPH [V][Nc]
-    const unsigned short* resid;  // identity residual, split planes [M][ldr]
-    long long resid_plane;
+    const unsigned short* resid;  // identity residual, SB [M][ldr]
     int ldr;
-    unsigned short* out_h;        // split output planes [M][ldo] (or null)
-    long long out_plane;
-    float* out_f;                 // fp32 output [M][ldo] (or null)
+    unsigned short* out_h;        // SB output [M][ldo] (or null)
     int ldo;
+    float* out_f;                 // fp32 output [M][ldf] (or null)
+    int ldf;
     const float* amix;            // EPI_GRAPH [V][V]
     int act;
     int mix_sparse;
-    const unsigned short* zeros;  // >= 16 B of zeros: source of padded rows
+    const unsigned short* zeros;  // >= 128 B of zeros: source of padded rows
     int tune;                     // tuning experiments (0 = production): 1 plain tile order
                                   // instead of the XCD-aware one
-    unsigned long long* trace;    // tuning only: per-workgroup {start, loop end, end, hw_id, xcc_id}
+    unsigned long long* trace;    // tuning only: per-workgroup {start, loop end, end, wait clk, barrier|loop clk}
 };
 
 enum Cgemm3Cfg {
@@ -62,14 +64,12 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st);
 bool tconv_halo_ok(const Cgemm3Args& a);
 hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st);
 
-// fp32 [rows][C] (row stride lds floats) -> split planes [rows][Cp] (zero-filled C..Cp)
-hipError_t launch_split(const float* x, long long rows, int C, int lds, int Cp, unsigned short* hi, long long plane,
-                        hipStream_t st);
-// split planes [rows][ld] -> fp32 [rows][C]
-hipError_t launch_merge(const unsigned short* hi, long long plane, long long rows, int C, int ld, float* y,
-                        hipStream_t st);
-// data_bn on load, straight to split planes with 8 channels (st_gcn_aaai18.py:119-125)
+// SB activations [rows][ld] -> fp32 [rows][C]
+hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st);
+// data_bn on load, straight to one SB block per pixel (C <= 32 channels, rest zero) (st_gcn_aaai18.py:119-125)
 hipError_t launch_data_bn_split(const float* x, int n_px, int V, int C, const float* scale, const float* shift,
-                                unsigned short* hi, long long plane, hipStream_t st);
+                                unsigned short* sb, hipStream_t st);
+
+inline int sb_blocks(int c) { return (c + 31) / 32; }
 
 }  // namespace tik

@@ -28,8 +28,8 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     constexpr int NW = WM * WN;                 // waves per workgroup
     constexpr int NT = 64 * NW;
     static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && (NW == 4 || NW == 8), "tile");
-    constexpr int R = 2 * BM + 2 * BN;          // image rows per stage
-    constexpr int NI = (R / 16 + NW - 1) / NW;  // DMA wave-instructions per wave per stage
+    constexpr int R = BM + BN;                  // 128-B image rows per stage (A rows, then B rows)
+    constexpr int NI = (R / 8 + NW - 1) / NW;   // DMA wave-instructions (8 rows each) per wave per stage
     constexpr int STAGEB = NI * NW * 1024;
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
@@ -65,20 +65,20 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     const int V = (VT > 0) ? VT : a.V;
     const unsigned long long ts0 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
 
-    // ---- per-lane DMA roles: instruction j covers image rows 16*(wave*NI+j) .. +15
+    // ---- per-lane DMA roles: instruction j covers image rows 8*(wave*NI+j) .. +7;
+    // lane l writes 16-B unit (l & 7) of row (l >> 3), fetching the source unit
+    // that the swizzle puts there
     int kind[NI], ck[NI], an[NI], at[NI], aw[NI], bcol[NI];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-        const int r = (wave * NI + j) * 16 + (lane >> 2);
-        int rr = r, k = 4;   // 0 A_hi, 1 A_lo, 2 B_hi, 3 B_lo, 4 pad
+        const int r = (wave * NI + j) * 8 + (lane >> 3);
+        int rr = r, k = 2;   // 0 A, 1 B, 2 pad
         if (r < BM) { k = 0; }
-        else if (r < 2 * BM) { k = 1; rr = r - BM; }
-        else if (r < 2 * BM + BN) { k = 2; rr = r - 2 * BM; }
-        else if (r < R) { k = 3; rr = r - 2 * BM - BN; }
-        ck[j] = (lane & 3) ^ sw3(rr);
+        else if (r < R) { k = 1; rr = r - BM; }
+        ck[j] = (lane & 7) ^ sbf(r);
         an[j] = at[j] = aw[j] = 0;
         bcol[j] = -1;
-        if (k <= 1) {
+        if (k == 0) {
             const int row = r0 + rr;
             if (row < a.M) {
                 const int q = row / V;
@@ -86,11 +86,11 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                 an[j] = q / a.tout;
                 at[j] = q - an[j] * a.tout;
             } else {
-                k = 4;
+                k = 2;
             }
-        } else if (k <= 3) {
+        } else if (k == 1) {
             bcol[j] = n0 + rr;
-            if (bcol[j] >= a.Nc) k = 4;
+            if (bcol[j] >= a.Nc) k = 2;
         }
         kind[j] = k;
     }
@@ -102,48 +102,45 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     if constexpr (EPI == EPI_GRAPH)
         for (int i = threadIdx.x; i < NA; i += NT) amix_s[i] = a.amix[i];
 
-    int ktotal = a.seg[0].kt * ((a.seg[0].cin8 + 31) / 32);
-    if (a.nseg > 1) ktotal += a.seg[1].kt * ((a.seg[1].cin8 + 31) / 32);
+    int ktotal = a.seg[0].kt * a.seg[0].nblk;
+    if (a.nseg > 1) ktotal += a.seg[1].kt * a.seg[1].nblk;
 
-    int seg = 0, tap = 0, c0 = 0, cin8 = 0;
+    // K cursor: (segment, tap, block); c0 = block * 64 halves
+    int seg = 0, tap = 0, c0 = 0;
     const unsigned short* base[NI];
     // segment fields by constant index only: a runtime-indexed kernarg struct
     // becomes vector loads + vmcnt(0) waits that would drain the DMA ring
     auto set_tap = [&]() {
         const Seg3 sg = (seg == 0) ? a.seg[0] : a.seg[1];
-        cin8 = sg.cin8;
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
             const unsigned short* p = nullptr;
-            if (kind[j] <= 1) {
+            if (kind[j] == 0) {
                 const int t = sg.stride * at[j] + tap - sg.pad;
-                if (t >= 0 && t < sg.tin)
-                    p = sg.src + (kind[j] ? sg.plane : 0) +
-                        (((long long)an[j] * sg.tin + t) * V + aw[j]) * sg.ld + 8 * ck[j];
-            } else if (kind[j] <= 3) {
-                p = (kind[j] == 2 ? sg.whi : sg.wlo) + (long long)bcol[j] * sg.ldw8 + tap * sg.cin8 + 8 * ck[j];
+                if (t >= 0 && t < sg.tin) p = sg.src + (((long long)an[j] * sg.tin + t) * V + aw[j]) * sg.ld + 8 * ck[j];
+            } else if (kind[j] == 1) {
+                p = sg.w + (long long)bcol[j] * sg.ldw + tap * sg.nblk * 64 + 8 * ck[j];
             }
             base[j] = p;
         }
     };
-    const int cin8_0 = a.seg[0].cin8, cin8_1 = a.seg[1].cin8, kt_0 = a.seg[0].kt, kt_1 = a.seg[1].kt;
+    const int nb_0 = a.seg[0].nblk * 64, nb_1 = a.seg[1].nblk * 64, kt_0 = a.seg[0].kt, kt_1 = a.seg[1].kt;
     auto advance = [&]() {
-        c0 += 32;
-        if (c0 >= (seg == 0 ? cin8_0 : cin8_1)) {
+        c0 += 64;
+        if (c0 >= (seg == 0 ? nb_0 : nb_1)) {
             c0 = 0;
             if (++tap >= (seg == 0 ? kt_0 : kt_1)) { tap = 0; ++seg; }
             if (seg < a.nseg) set_tap();
         }
     };
-    auto issue_part = [&](int slot, int j0, int j1) {
+    auto issue = [&](int slot) {
         unsigned char* dst = smem + slot * STAGEB + wave * NI * 1024;
 #pragma unroll
-        for (int j = j0; j < j1; ++j) {
-            const unsigned short* p = (base[j] && c0 + 8 * ck[j] < cin8) ? base[j] + c0 : a.zeros;
+        for (int j = 0; j < NI; ++j) {
+            const unsigned short* p = base[j] ? base[j] + c0 : a.zeros;
             if (DBG != 2) __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
-    auto issue = [&](int slot) { issue_part(slot, 0, NI); };
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -156,22 +153,19 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     const int g = lane >> 4;
     auto compute = [&](int slot) {
         if (DBG == 1) return;
-        const unsigned char* Ahi = smem + slot * STAGEB;
-        const unsigned char* Alo = Ahi + BM * 64;
-        const unsigned char* Bhi = Alo + BM * 64;
-        const unsigned char* Blo = Bhi + BN * 64;
+        const unsigned char* img = smem + slot * STAGEB;
         f16x8 bh[FN], bl[FN];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-            const int off = swz3(brow + j * 16, g);
-            bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
-            bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
+            const int r = BM + brow + j * 16;
+            bh[j] = *reinterpret_cast<const f16x8*>(img + sbo(r, g));
+            bl[j] = *reinterpret_cast<const f16x8*>(img + sbo(r, 4 + g));
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-            const int off = swz3(arow + i * 16, g);
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
+            const int r = arow + i * 16;
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(img + sbo(r, g));
+            const f16x8 al = *reinterpret_cast<const f16x8*>(img + sbo(r, 4 + g));
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
@@ -268,7 +262,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                 f32x4 y[VT];
 #pragma unroll
                 for (int v = 0; v < VT; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * VT + v) * LDC + 4 * c4);
-                const size_t obase = (size_t)(frame0 + f) * VT * a.ldo + col;
+                const size_t obase = (size_t)(frame0 + f) * VT * a.ldo;
                 const bool full = col + 3 < a.Nc;
 #pragma unroll
                 for (int w = 0; w < VT; ++w) {
@@ -281,15 +275,16 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                     if (full) {
                         f16x4 h, l;
                         split4(z, h, l);
-                        unsigned short* o = a.out_h + obase + (size_t)w * a.ldo;
+                        unsigned short* o = a.out_h + obase + (size_t)w * a.ldo + sbc(col);
                         *reinterpret_cast<f16x4*>(o) = h;
-                        *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
+                        *reinterpret_cast<f16x4*>(o + 32) = l;
                     } else {
                         for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
                             const _Float16 h = (_Float16)z[e];
                             const _Float16 l = (_Float16)(z[e] - (float)h);
-                            a.out_h[obase + (size_t)w * a.ldo + e] = __builtin_bit_cast(unsigned short, h);
-                            a.out_h[obase + (size_t)w * a.ldo + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                            unsigned short* o = a.out_h + obase + (size_t)w * a.ldo + sbc(col + e);
+                            o[0] = __builtin_bit_cast(unsigned short, h);
+                            o[32] = __builtin_bit_cast(unsigned short, l);
                         }
                     }
                 }
@@ -321,7 +316,10 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     if (!a.zeros) return hipErrorInvalidValue;
     for (int s = 0; s < a.nseg; ++s)
-        if (a.seg[s].cin8 % 8 || a.seg[s].ld % 8 || !a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+        if (a.seg[s].nblk <= 0 || a.seg[s].ld % 8 || a.seg[s].ld < 64 * a.seg[s].nblk || !a.seg[s].w ||
+            a.seg[s].ldw < a.seg[s].kt * a.seg[s].nblk * 64)
+            return hipErrorInvalidValue;
+    if (a.out_h && (a.ldo % 8 || a.ldo < 64 * sb_blocks(a.Nc))) return hipErrorInvalidValue;
     (void)hipGetLastError();
     switch (cfg) {
         case C3_T128x128: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2>(a, st);
@@ -351,32 +349,18 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- conversions
-__global__ void split_kernel(const float* __restrict__ x, long long rows, int C, int lds, int Cp,
-                             unsigned short* __restrict__ hi, long long plane) {
-    const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= rows * Cp) return;
-    const long long r = p / Cp;
-    const int c = (int)(p - r * Cp);
-    const float v = c < C ? x[r * lds + c] : 0.f;
-    const _Float16 h = (_Float16)v;
-    const _Float16 l = (_Float16)(v - (float)h);
-    hi[p] = __builtin_bit_cast(unsigned short, h);
-    hi[p + plane] = __builtin_bit_cast(unsigned short, l);
-}
-
-__global__ void merge_kernel(const unsigned short* __restrict__ hi, long long plane, long long rows, int C, int ld,
-                             float* __restrict__ y) {
+__global__ void merge_kernel(const unsigned short* __restrict__ sb, long long rows, int C, int ld, float* __restrict__ y) {
     const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= rows * C) return;
     const long long r = p / C;
     const int c = (int)(p - r * C);
-    const size_t i = (size_t)r * ld + c;
-    y[p] = (float)__builtin_bit_cast(_Float16, hi[i]) + (float)__builtin_bit_cast(_Float16, hi[i + plane]);
+    const unsigned short* q = sb + (size_t)r * ld + ((c >> 5) << 6) + (c & 31);
+    y[p] = (float)__builtin_bit_cast(_Float16, q[0]) + (float)__builtin_bit_cast(_Float16, q[32]);
 }
 
-// x (px, C<=4) -> split planes (px, 8): per-(v,c) eval BN (channel v*C + c)
+// x (px, C<=32) -> one SB block per pixel: per-(v,c) eval BN (channel v*C + c)
 __global__ void data_bn_split_kernel(const float* __restrict__ x, int n_px, int V, int C, const float* __restrict__ scale,
-                                     const float* __restrict__ shift, unsigned short* __restrict__ hi, long long plane) {
+                                     const float* __restrict__ shift, unsigned short* __restrict__ sb) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_px) return;
     const int v = p % V;
@@ -386,34 +370,26 @@ __global__ void data_bn_split_kernel(const float* __restrict__ x, int n_px, int 
         h[c] = (_Float16)t;
         l[c] = (_Float16)(t - (float)h[c]);
     }
-    *reinterpret_cast<f16x8*>(hi + (size_t)p * 8) = h;
-    *reinterpret_cast<f16x8*>(hi + (size_t)p * 8 + plane) = l;
+    f16x8* o = reinterpret_cast<f16x8*>(sb + (size_t)p * 64);
+    const f16x8 z = {};
+    o[0] = h; o[1] = z; o[2] = z; o[3] = z;
+    o[4] = l; o[5] = z; o[6] = z; o[7] = z;
 }
 
-hipError_t launch_split(const float* x, long long rows, int C, int lds, int Cp, unsigned short* hi, long long plane,
-                        hipStream_t st) {
-    const long long n = rows * Cp;
-    if (n <= 0) return hipSuccess;
-    (void)hipGetLastError();
-    hipLaunchKernelGGL(split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows, C, lds, Cp, hi, plane);
-    return hipGetLastError();
-}
-
-hipError_t launch_merge(const unsigned short* hi, long long plane, long long rows, int C, int ld, float* y,
-                        hipStream_t st) {
+hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st) {
     const long long n = rows * C;
     if (n <= 0) return hipSuccess;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, hi, plane, rows, C, ld, y);
+    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sb, rows, C, ld, y);
     return hipGetLastError();
 }
 
 hipError_t launch_data_bn_split(const float* x, int n_px, int V, int C, const float* scale, const float* shift,
-                                unsigned short* hi, long long plane, hipStream_t st) {
+                                unsigned short* sb, hipStream_t st) {
     if (n_px <= 0) return hipSuccess;
+    if (C > 8) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(data_bn_split_kernel, dim3((n_px + 255) / 256), dim3(256), 0, st, x, n_px, V, C, scale, shift, hi,
-                       plane);
+    hipLaunchKernelGGL(data_bn_split_kernel, dim3((n_px + 255) / 256), dim3(256), 0, st, x, n_px, V, C, scale, shift, sb);
     return hipGetLastError();
 }
 

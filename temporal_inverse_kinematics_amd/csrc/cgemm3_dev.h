@@ -1,6 +1,7 @@
-// cgemm3_dev.h — device helpers shared by the split-activation f16x3 kernels
-// (cgemm3.hip, tconv.hip): vector types, the 64-B-row LDS swizzle, f16 hi/lo
-// splitting, and the bias/residual/activation epilogue of a staged C tile.
+// cgemm3_dev.h — device helpers shared by the split-block f16x3 kernels
+// (cgemm3.hip, tconv.hip): vector types, the 128-B-row LDS swizzle of the
+// split-block image, f16 hi/lo splitting, and the bias/residual/activation
+// epilogue of a staged C tile.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -18,8 +19,15 @@ __host__ __device__ constexpr unsigned coco_hop2_mask3(int w) {
     return m[w];
 }
 
-__device__ __forceinline__ int sw3(int r) { return (0x1230 >> (4 * ((r >> 2) & 3))) & 3; }
-__device__ __forceinline__ int swz3(int r, int c) { return r * 64 + ((c ^ sw3(r)) << 4); }
+// LDS image of one K block: 128-B rows (8 x 16-B units: hi k 0-7, 8-15,
+// 16-23, 24-31, then lo likewise); unit u of row r sits at u ^ ((r >> 1) & 7).
+// A 16-row fragment read (ds_read_b128, fixed unit) then touches 16 distinct
+// 16-B bank slots: conflict-free.
+__device__ __forceinline__ int sbf(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int sbo(int r, int u) { return r * 128 + ((u ^ sbf(r)) << 4); }
+
+// element offset of channel c (4-aligned group start) in an SB row
+__device__ __forceinline__ int sbc(int c) { return ((c >> 5) << 6) + (c & 31); }
 
 __device__ __forceinline__ void split4(const f32x4 v, f16x4& h, f16x4& l) {
 #pragma unroll
@@ -29,23 +37,17 @@ __device__ __forceinline__ void split4(const f32x4 v, f16x4& h, f16x4& l) {
     }
 }
 
-__device__ __forceinline__ f32x4 merge4(const unsigned short* hi, long long plane) {
-    const f16x4 h = *reinterpret_cast<const f16x4*>(hi);
-    const f16x4 l = *reinterpret_cast<const f16x4*>(hi + plane);
-    f32x4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (float)h[e] + (float)l[e];
-    return v;
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // Bias epilogue of a BM x BN fp32 tile staged in LDS (row stride LDC floats):
-// v = act(C + bias + residual) -> split planes and/or fp32. bv = this
-// thread's 4 bias values (columns n0 + 4*(tid % (BN/4)) ...), zero past Nc.
+// v = act(C + bias + residual) -> SB output and/or fp32. bv = this thread's 4
+// bias values (columns n0 + 4*(tid % (BN/4)) ...), zero past Nc. All residual
+// loads are issued before any store, and the math between stores is
+// branch-free (a data-dependent branch between stores makes the compiler wait
+// for every outstanding store: vmcnt counts stores too).
 template <int BM, int BN, int NT, int LDC>
 __device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, const f32x4 bv, int r0, int n0, int tid) {
     constexpr int C4 = BN / 4;
@@ -54,11 +56,8 @@ __device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, c
     constexpr int KI = BM / RS;          // items per thread
     const int c4 = tid % C4, lr0 = tid / C4;
     const int col = n0 + 4 * c4;
-    const bool vec = (a.ldo % 4 == 0) && (!a.resid || a.ldr % 4 == 0) && col + 3 < a.Nc;
-    if (vec) {
-        // all residual loads first, then branch-free math and the stores
-        // (a data-dependent branch between stores makes the compiler wait
-        // for every outstanding store: vmcnt counts stores too)
+    const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
+    if (col + 3 < a.Nc) {
         f16x4 rh[KI], rl[KI];
 #pragma unroll
         for (int k = 0; k < KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
@@ -67,13 +66,12 @@ __device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, c
             for (int k = 0; k < KI; ++k) {
                 const int row = r0 + lr0 + k * RS;
                 if (row < a.M) {
-                    const unsigned short* rp = a.resid + (size_t)row * a.ldr + col;
+                    const unsigned short* rp = a.resid + (size_t)row * a.ldr + sbc(col);
                     rh[k] = *reinterpret_cast<const f16x4*>(rp);
-                    rl[k] = *reinterpret_cast<const f16x4*>(rp + a.resid_plane);
+                    rl[k] = *reinterpret_cast<const f16x4*>(rp + 32);
                 }
             }
         }
-        const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const int lr = lr0 + k * RS, row = r0 + lr;
@@ -87,31 +85,39 @@ __device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, c
             if (a.out_h) {
                 f16x4 h, l;
                 split4(v, h, l);
-                unsigned short* o = a.out_h + (size_t)row * a.ldo + col;
+                unsigned short* o = a.out_h + (size_t)row * a.ldo + sbc(col);
                 *reinterpret_cast<f16x4*>(o) = h;
-                *reinterpret_cast<f16x4*>(o + a.out_plane) = l;
+                *reinterpret_cast<f16x4*>(o + 32) = l;
             }
-            if (a.out_f) *reinterpret_cast<f32x4*>(a.out_f + (size_t)row * a.ldo + col) = v;
+            if (a.out_f) {
+                float* of = a.out_f + (size_t)row * a.ldf + col;
+                if ((a.ldf & 3) == 0) {
+                    *reinterpret_cast<f32x4*>(of) = v;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) of[e] = v[e];
+                }
+            }
         }
-    } else {
+    } else if (col < a.Nc) {
+        // ragged last column group (fp32 outputs only, e.g. the 66 pose values)
         for (int k = 0; k < KI; ++k) {
             const int lr = lr0 + k * RS, row = r0 + lr;
             if (row >= a.M) continue;
             for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
                 float v = Cs[lr * LDC + 4 * c4 + e] + bv[e];
                 if (a.resid) {
-                    const unsigned short* rp = a.resid + (size_t)row * a.ldr + col + e;
-                    v += (float)__builtin_bit_cast(_Float16, rp[0]) + (float)__builtin_bit_cast(_Float16, rp[a.resid_plane]);
+                    const unsigned short* rp = a.resid + (size_t)row * a.ldr + sbc(col + e);
+                    v += (float)__builtin_bit_cast(_Float16, rp[0]) + (float)__builtin_bit_cast(_Float16, rp[32]);
                 }
-                if (a.act == ACT_RELU) v = v > 0.f ? v : 0.f;
-                else if (a.act == ACT_LEAKY) v = v > 0.f ? v : 0.01f * v;
+                v = v > 0.f ? v : slope * v;
                 if (a.out_h) {
                     const _Float16 h = (_Float16)v;
                     const _Float16 l = (_Float16)(v - (float)h);
-                    a.out_h[(size_t)row * a.ldo + col + e] = __builtin_bit_cast(unsigned short, h);
-                    a.out_h[(size_t)row * a.ldo + col + e + a.out_plane] = __builtin_bit_cast(unsigned short, l);
+                    a.out_h[(size_t)row * a.ldo + sbc(col + e)] = __builtin_bit_cast(unsigned short, h);
+                    a.out_h[(size_t)row * a.ldo + sbc(col + e) + 32] = __builtin_bit_cast(unsigned short, l);
                 }
-                if (a.out_f) a.out_f[(size_t)row * a.ldo + col + e] = v;
+                if (a.out_f) a.out_f[(size_t)row * a.ldf + col + e] = v;
             }
         }
     }

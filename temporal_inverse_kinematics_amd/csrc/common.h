@@ -128,6 +128,30 @@ struct SplitW {
     }
 };
 
+// Split-block ("SB") weights for cgemm3.hip: w[n][tap*cin + ci] (row stride
+// ldw floats) -> [Nc][kt][nblk][64] halves, each 32-channel block stored as
+// [hi(w) x32 | lo(w) = f16(w - hi) x32], zero-padded to whole blocks.
+struct SBW {
+    DevHBuf w;
+    int nblk = 0, ldw = 0;
+    int build(const std::vector<float>& src, int Nc, int kt, int cin, int ldw_src) {
+        nblk = (cin + 31) / 32;
+        ldw = kt * nblk * 64;
+        std::vector<unsigned short> h((size_t)Nc * ldw, 0);
+        for (int n = 0; n < Nc; ++n)
+            for (int t = 0; t < kt; ++t)
+                for (int c = 0; c < cin; ++c) {
+                    const float x = src[(size_t)n * ldw_src + (size_t)t * cin + c];
+                    const _Float16 xh = (_Float16)x;
+                    const _Float16 xl = (_Float16)(x - (float)xh);
+                    const size_t o = (size_t)n * ldw + (size_t)t * nblk * 64 + (size_t)(c / 32) * 64 + c % 32;
+                    h[o] = __builtin_bit_cast(unsigned short, xh);
+                    h[o + 32] = __builtin_bit_cast(unsigned short, xl);
+                }
+        return w.upload(h);
+    }
+};
+
 // default arithmetic of the GEMMs: TIK_PRECISION=fp32 selects the exact f32
 // MFMA path; anything else the 3-term f16 split (cgemm.hip)
 inline int default_precision() {

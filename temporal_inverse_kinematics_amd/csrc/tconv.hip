@@ -26,10 +26,10 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
     constexpr int HMAX = 192;             // halo rows in the image (>= 11 frames x 17)
     constexpr int ZR = HMAX - 1;          // a row that is always zero-filled
-    constexpr int ASLOT = 2 * HMAX * 64;  // hi + lo planes, 64-B rows
-    constexpr int BSLOT = 2 * BN * 64;
-    constexpr int NIA = 2 * HMAX / 16 / 4;   // halo DMA wave-instructions per wave
-    constexpr int NIB = 2 * BN / 16 / 4;     // weight DMA wave-instructions per wave
+    constexpr int ASLOT = HMAX * 128;     // split-block rows: 128 B = 32 channels hi | lo
+    constexpr int BSLOT = BN * 128;
+    constexpr int NIA = HMAX / 8 / 4;     // halo DMA wave-instructions (8 rows each) per wave
+    constexpr int NIB = BN / 8 / 4;       // weight DMA wave-instructions per wave
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
     constexpr int RING = 2 * ASLOT + 2 * BSLOT;
@@ -72,23 +72,20 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
         if (r < M && t + 1 < tin) tapok |= 2u << (2 * i);
     }
 
-    // DMA roles. Halo instruction j: image row ir -> plane ir / HMAX, halo row ir % HMAX.
-    int a_row[NIA], a_ck[NIA], a_pl[NIA];
+    // DMA roles: instruction j covers 8 image rows; lane l writes unit l & 7 of
+    // row l >> 3 and fetches the source unit the swizzle puts there
+    int a_row[NIA], a_ck[NIA];
 #pragma unroll
     for (int j = 0; j < NIA; ++j) {
-        const int ir = (wave * NIA + j) * 16 + (lane >> 2);
-        const int hrow = ir % HMAX;
-        a_pl[j] = ir / HMAX;
-        a_ck[j] = (lane & 3) ^ sw3(hrow);
+        const int hrow = (wave * NIA + j) * 8 + (lane >> 3);
+        a_ck[j] = (lane & 7) ^ sbf(hrow);
         a_row[j] = hrow < HR ? F0 * V + hrow : -1;
     }
-    int b_col[NIB], b_ck[NIB], b_pl[NIB];
+    int b_col[NIB], b_ck[NIB];
 #pragma unroll
     for (int j = 0; j < NIB; ++j) {
-        const int ir = (wave * NIB + j) * 16 + (lane >> 2);
-        const int rr = ir % BN;
-        b_pl[j] = ir / BN;
-        b_ck[j] = (lane & 3) ^ sw3(rr);
+        const int rr = (wave * NIB + j) * 8 + (lane >> 3);
+        b_ck[j] = (lane & 7) ^ sbf(rr);
         b_col[j] = n0 + rr < a.Nc ? n0 + rr : -1;
     }
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -100,33 +97,31 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
     }
 
     // iteration space: segment 0 (taps 0,1,2 per chunk), segment 1 (centre tap)
-    const int G0 = (a.seg[0].cin8 + 31) / 32;
-    const int G1 = a.nseg > 1 ? (a.seg[1].cin8 + 31) / 32 : 0;
+    const int G0 = a.seg[0].nblk;
+    const int G1 = a.nseg > 1 ? a.seg[1].nblk : 0;
     const int NIT = 3 * G0 + G1;
 
     auto issue_halo = [&](int grp, int slot, int j0, int j1) {
         const bool s1 = grp >= G0;
         const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
-        const int c0 = 32 * (s1 ? grp - G0 : grp);
+        const int c0 = 64 * (s1 ? grp - G0 : grp);
         unsigned char* dst = smem + slot * ASLOT + wave * NIA * 1024;
 #pragma unroll
         for (int j = j0; j < j1; ++j) {
             const unsigned short* p = a.zeros;
-            if (a_row[j] >= 0 && c0 + 8 * a_ck[j] < sg.cin8)
-                p = sg.src + (a_pl[j] ? sg.plane : 0) + (long long)a_row[j] * sg.ld + c0 + 8 * a_ck[j];
+            if (a_row[j] >= 0) p = sg.src + (long long)a_row[j] * sg.ld + c0 + 8 * a_ck[j];
             __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
     auto issue_w = [&](int grp, int tap, int slot, int j0, int j1) {
         const bool s1 = grp >= G0;
         const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
-        const int c0 = 32 * (s1 ? grp - G0 : grp);
+        const int c0 = 64 * (s1 ? grp - G0 : grp);
         unsigned char* dst = smem + 2 * ASLOT + slot * BSLOT + wave * NIB * 1024;
 #pragma unroll
         for (int j = j0; j < j1; ++j) {
             const unsigned short* p = a.zeros;
-            if (b_col[j] >= 0 && c0 + 8 * b_ck[j] < sg.cin8)
-                p = (b_pl[j] ? sg.wlo : sg.whi) + (long long)b_col[j] * sg.ldw8 + (s1 ? 0 : tap) * sg.cin8 + c0 + 8 * b_ck[j];
+            if (b_col[j] >= 0) p = sg.w + (long long)b_col[j] * sg.ldw + (s1 ? 0 : tap) * sg.nblk * 64 + c0 + 8 * b_ck[j];
             __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
@@ -137,37 +132,26 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int brow = wn * FN * 16 + (lane & 15);
-    // MFMAs of one iteration, with the next iteration's DMAs (gn >= 0: weight
-    // tile of group gn / tap tn; hnew: also the halo of group gn) spread
-    // between the fragment groups
-    auto compute = [&](int aslot, int bslot, int tap, int gn, int tn, bool hnew) {
-        const unsigned char* Ahi = smem + aslot * ASLOT;
-        const unsigned char* Alo = Ahi + HMAX * 64;
-        const unsigned char* Bhi = smem + 2 * ASLOT + bslot * BSLOT;
-        const unsigned char* Blo = Bhi + BN * 64;
+    auto compute = [&](int aslot, int bslot, int tap) {
+        const unsigned char* Aimg = smem + aslot * ASLOT;
+        const unsigned char* Bimg = smem + 2 * ASLOT + bslot * BSLOT;
         f16x8 bh[FN], bl[FN];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-            const int off = swz3(brow + j * 16, g);
-            bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
-            bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
+            bh[j] = *reinterpret_cast<const f16x8*>(Bimg + sbo(brow + j * 16, g));
+            bl[j] = *reinterpret_cast<const f16x8*>(Bimg + sbo(brow + j * 16, 4 + g));
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
             int hr = hr1[i];
             if (tap != 1) hr = ((tapok >> (2 * i + (tap >> 1))) & 1u) ? hr + (tap - 1) * V : ZR;
-            const int off = swz3(hr, g);
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(Aimg + sbo(hr, g));
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Aimg + sbo(hr, 4 + g));
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
-            }
-            if (gn >= 0) {
-                issue_w(gn, tn, bslot ^ 1, (i * NIB) / FM, ((i + 1) * NIB) / FM);
-                if (hnew) issue_halo(gn, gn & 1, (i * NIA) / FM, ((i + 1) * NIA) / FM);
             }
         }
     };
@@ -191,8 +175,12 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
                 tw_vm += w1 - w0; tw_bar += w2 - w1;
             }
             const int grp = it_group(it);
-            const int gn = it + 1 < NIT ? it_group(it + 1) : -1;
-            compute(grp & 1, it & 1, it_tap(it), gn, it + 1 < NIT ? it_tap(it + 1) : 0, gn >= 0 && gn != grp);
+            if (it + 1 < NIT) {
+                const int gn = it_group(it + 1);
+                if (gn != grp) issue_halo(gn, gn & 1, 0, NIA);
+                issue_w(gn, it_tap(it + 1), (it + 1) & 1, 0, NIB);
+            }
+            compute(grp & 1, it & 1, it_tap(it));
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -238,7 +226,8 @@ hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     if (!tconv_halo_ok(a) || (bn != 64 && bn != 128)) return hipErrorInvalidValue;
     for (int s = 0; s < a.nseg; ++s)
-        if (a.seg[s].cin8 % 8 || a.seg[s].ld % 8 || !a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+        if (a.seg[s].nblk <= 0 || a.seg[s].ld % 8 || a.seg[s].ld < 64 * a.seg[s].nblk || !a.seg[s].w) return hipErrorInvalidValue;
+    if (a.out_h && (a.ldo % 8 || a.ldo < 64 * sb_blocks(a.Nc))) return hipErrorInvalidValue;
     (void)hipGetLastError();
     const dim3 grid((a.M + 127) / 128, (a.Nc + bn - 1) / bn), blk(256);
     if (bn == 128) hipLaunchKernelGGL(tconv_halo_kernel<128>, grid, blk, 0, st, a);

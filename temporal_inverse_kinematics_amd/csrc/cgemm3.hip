@@ -29,8 +29,11 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     constexpr int NT = 64 * NW;
     static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN && (NW == 4 || NW == 8), "tile");
     constexpr int R = BM + BN;                  // 128-B image rows per stage (A rows, then B rows)
-    constexpr int NI = (R / 8 + NW - 1) / NW;   // DMA wave-instructions (8 rows each) per wave per stage
-    constexpr int STAGEB = NI * NW * 1024;
+    static_assert(R % 8 == 0, "image rows");
+    constexpr int NIT = R / 8;                  // DMA wave-instructions (8 rows each) per stage
+    constexpr int NI = (NIT + NW - 1) / NW;     // ... per wave (the last waves may issue fewer)
+    constexpr int PN = NIT % NI;                // count of a partial wave (0: none)
+    constexpr int STAGEB = NIT * 1024;
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
     constexpr int SMEM = NSTAGE * STAGEB > CTILE ? NSTAGE * STAGEB : CTILE;
@@ -138,7 +141,8 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
             const unsigned short* p = base[j] ? base[j] + c0 : a.zeros;
-            if (DBG != 2) __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+            if (DBG != 2 && (NIT % NW == 0 || wave * NI + j < NIT))
+                __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
         }
     };
 
@@ -208,9 +212,19 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             // stages' NI-instruction groups are still outstanding
             const int ahead = min(NSTAGE - 2, ktotal - 1 - ch);
             const unsigned long long w0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
-            if (NSTAGE >= 4 && ahead >= 2) wait_vm<(NSTAGE >= 4 ? 2 * NI : 0)>();
-            else if (NSTAGE >= 3 && ahead >= 1) wait_vm<(NSTAGE >= 3 ? NI : 0)>();
-            else wait_vm<0>();
+            // this wave's DMA count per stage: NI, PN (one partial wave) or 0
+            const int myn = min(NI, max(0, NIT - wave * NI));
+            if (NSTAGE >= 4 && ahead >= 2) {
+                if (myn == NI) wait_vm<(NSTAGE >= 4 ? 2 * NI : 0)>();
+                else if (myn == PN) wait_vm<(NSTAGE >= 4 ? 2 * PN : 0)>();
+                else wait_vm<0>();
+            } else if (NSTAGE >= 3 && ahead >= 1) {
+                if (myn == NI) wait_vm<(NSTAGE >= 3 ? NI : 0)>();
+                else if (myn == PN) wait_vm<(NSTAGE >= 3 ? PN : 0)>();
+                else wait_vm<0>();
+            } else {
+                wait_vm<0>();
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const unsigned long long w1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
             __builtin_amdgcn_s_barrier();
@@ -336,7 +350,7 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
         case C3_T128x64_S4: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 4>(a, st);
         case C3_G272x128_W8:
             if (a.V != 17) return hipErrorInvalidValue;
-            return launch3<272, 128, 1, 8, EPI_GRAPH, 17, 2>(a, st);
+            return launch3<272, 128, 1, 8, EPI_GRAPH, 17, 3>(a, st);
         case C3_DBG_T128x128_DMA: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2, 1>(a, st);
         case C3_DBG_T128x128_MFMA: return launch3<128, 128, 2, 2, EPI_BIAS, 0, 2, 2>(a, st);
         case C3_DBG_T128x64_DMA: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 3, 1>(a, st);

@@ -29,6 +29,34 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-in MFMA (= f32 
 F16_MFMA_PEAK_TFLOPS = 2516.6   # 1024 FLOP/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz (~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 
+# profiler label prefix (csrc/api.cpp ProfScope) -> kernel symbol in rocprofv3 output
+KERNEL_SYMBOLS = {
+    "G3_272x128": "tik::cgemm3_kernel<272, 128, 1, 8, 1, 17, 3, 0>",
+    "G3_272x64": "tik::cgemm3_kernel<272, 64, 1, 4, 1, 17, 1, 0>",
+    "T3_128x128": "tik::cgemm3_kernel<128, 128, 2, 2, 0, 0, 2, 0>",
+    "T3_128x64": "tik::cgemm3_kernel<128, 64, 2, 2, 0, 0, 3, 0>",
+    "TH_128x128": "tik::tconv_halo_kernel<128>",
+    "TH_128x64": "tik::tconv_halo_kernel<64>",
+    "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",
+}
+
+
+def _pmc_traffic(path, label):
+    """HBM bytes per dispatch of the kernel behind `label` from a PMC summary
+    (scripts/pmc_traffic.py output), or None."""
+    import glob
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")), key=os.path.getmtime)
+        path = cands[-1] if cands else None
+    if not path or not os.path.exists(path):
+        return None, None
+    sym = KERNEL_SYMBOLS.get(label)
+    kern = json.load(open(path)).get("kernels", {})
+    for k, v in kern.items():
+        if sym and k.replace("void ", "").strip() == sym:
+            return v["hbm_bytes_per_dispatch"], os.path.relpath(path, REPO)
+    return None, os.path.relpath(path, REPO)
+
 
 def _cpu_baseline(T: int, seconds: float = 12.0):
     """Oracle (numpy fp32, the reference algorithm unfused) on a bounded sample."""
@@ -64,6 +92,8 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
                     help="GEMM arithmetic: 3-term f16 split MFMA (default) or exact fp32 MFMA")
     ap.add_argument("--no-compare", action="store_true", help="skip the second-precision comparison run")
+    ap.add_argument("--pmc-traffic", default=None,
+                    help="PMC traffic summary (scripts/pmc_traffic.py); default: newest profiles/*pmc_traffic*.json")
     args = ap.parse_args()
 
     import numpy as np
@@ -167,14 +197,22 @@ def main():
         dom = max(agg, key=lambda k: agg[k][0])
         tot_ms, cnt, tot_fl, tot_by = agg[dom]
         avg_s = tot_ms / cnt / 1e3
-        achieved = tot_fl / cnt / avg_s / 1e12
+        tflops = tot_fl / cnt / avg_s / 1e12
+        gbs = tot_by / cnt / avg_s / 1e9
         if args.precision == "f16x3":
-            peak = F16_MFMA_PEAK_TFLOPS / 3
+            mpeak = F16_MFMA_PEAK_TFLOPS / 3
             basis = ("fp32-equivalent ceiling of the 3-term f16 split: dense f16 MFMA 2516.6 TF / 3 "
                      "MFMAs per fp32 product; executed MFMA TF/s = 3 x achieved")
         else:
-            peak = FP32_MFMA_PEAK_TFLOPS
+            mpeak = FP32_MFMA_PEAK_TFLOPS
             basis = "dense fp32 MFMA (v_mfma_f32_16x16x4_f32) peak"
+        # the binding roof is the one the kernel is closer to
+        if gbs / HBM_PEAK_GBS > tflops / mpeak:
+            bound, achieved, peak, unit = "hbm", gbs, HBM_PEAK_GBS, "GB/s"
+            basis = "HBM3E spec peak; achieved = algorithmic bytes (4 B per activation element read/written once)"
+        else:
+            bound, achieved, peak, unit = "mfma", tflops, mpeak, "TFLOP/s"
+        traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom)
         kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
                        "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 2), "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1)}
                    for k, v in agg.items()}
@@ -196,12 +234,16 @@ def main():
                                    f"SMPL-X pose" + (f", RCCL all-gather of poses over {world} GPUs" if world > 1 else ""),
                        "global_batch": world * B, "window_frames": T, "out_frames": Tp,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
-            "roofline": {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2),
-                         "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "peak_basis": basis,
-                         "traffic": None,
-                         "hbm_gbs_algorithmic": round(tot_by / cnt / avg_s / 1e9, 1),
-                         "hbm_frac_algorithmic": round(tot_by / cnt / avg_s / 1e9 / HBM_PEAK_GBS, 5)},
+            "roofline": {"kernel": dom, "symbol": KERNEL_SYMBOLS.get(dom), "bound": bound,
+                         "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
+                         "frac": round(achieved / peak, 4), "peak_basis": basis,
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": round(tot_by / cnt),
+                         "algorithmic_flops_per_launch": round(tot_fl / cnt),
+                         "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
+                         "tflops": round(tflops, 2), "gbs_algorithmic": round(gbs, 1)},
             "forward": {"algorithmic_tflops": round(fwd_flops * args.steps / dt / 1e12, 2),
                         "mflop_per_window": round(fwd_flops / B / 1e6, 2), "kernels": kernels,
                         "launches": {k: {"avg_ms": round(v[0] / v[1], 4), "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 1),

@@ -113,8 +113,13 @@ int main(int argc, char** argv) {
     float* amix = dev_floats(V * V, 0.05f);
     int tin = T0;
     double tot_best = 0, tot_cur = 0;
+    const int only = argc > 4 ? atoi(argv[4]) : -1;   // profile one layer only
     for (int l = 0; l < 8; ++l) {
         const L& Ly = layers[l];
+        if (only >= 0 && l != only) {
+            tin = (tin - 1) / Ly.stride + 1;
+            continue;
+        }
         const int to = (tin - 1) / Ly.stride + 1;
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         tik::Cgemm3Args g{};

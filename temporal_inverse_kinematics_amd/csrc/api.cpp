@@ -316,6 +316,7 @@ struct tik_model {
     DevBuf part;                   // split-K partial sums (small-batch launches)
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
+    int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
     Profiler prof;
     bool profiling = false;
 };
@@ -405,6 +406,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         delete md;
         return rc;
     }
+    if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
         else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
@@ -451,6 +453,23 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
 
 static bool use_dma(const tik_model* m, int N, int T) {
     return m->prec == tik::PREC_F16X3 && m->dma_min_frames > 0 && (long long)N * T >= m->dma_min_frames;
+}
+
+// Windows per DMA-path call: the kernels address each activation tensor with
+// 32-bit buffer offsets (out-of-range = zero fill), so every SB tensor of one
+// call must stay below 2 GiB; larger batches run as independent sub-batches.
+static int dma_chunk(const tik_model* m, int T) {
+    long long worst = (long long)T * m->V * 64 * 2;   // layer-0 input block
+    int t = T;
+    for (const Layer& L : m->layers) {
+        const long long row = 64LL * L.sbt.nblk * 2;   // bytes per SB row of cout channels
+        worst = std::max(worst, (long long)t * m->V * row);   // z
+        t = Layer::tout(t, L.stride);
+        worst = std::max(worst, (long long)t * m->V * row);   // out
+    }
+    const long long lim = (1LL << 31) - (1LL << 20);
+    const int c = (int)std::max(1LL, lim / worst);
+    return m->dma_chunk_max > 0 ? std::min(c, m->dma_chunk_max) : c;
 }
 
 // Backbone on fp32 activations (both precisions; split-K for small batches).
@@ -508,15 +527,20 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     hipStream_t st = (hipStream_t)stream;
     ProfGuard pg(m);
     int to, rc;
-    if ((rc = tik_model_reserve(m, N, T))) return rc;
     if (use_dma(m, N, T)) {
-        const half_t* f;
-        int ld;
-        if ((rc = backbone3(m, x, N, T, &f, &ld, &to, st))) return rc;
-        const int C = m->layers.back().cout;
-        HIP_TRY(tik::launch_merge(f, (long long)N * to * m->V, C, ld, feat, st));
+        const int chunk = std::min(N, dma_chunk(m, T));
+        if ((rc = tik_model_reserve(m, chunk, T))) return rc;
+        for (int n0 = 0; n0 < N; n0 += chunk) {
+            const int n = std::min(chunk, N - n0);
+            const half_t* f;
+            int ld;
+            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st))) return rc;
+            const int C = m->layers.back().cout;
+            HIP_TRY(tik::launch_merge(f, (long long)n * to * m->V, C, ld, feat + (size_t)n0 * to * m->feat, st));
+        }
         return TIK_OK;
     }
+    if ((rc = tik_model_reserve(m, N, T))) return rc;
     float* f;
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
     HIP_TRY(hipMemcpyAsync(feat, f, sizeof(float) * (size_t)N * to * m->feat, hipMemcpyDeviceToDevice, st));
@@ -557,13 +581,19 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     ProfGuard pg(m);
     float* f;
     int to, rc;
-    if ((rc = tik_model_reserve(m, N, T))) return rc;
     if (use_dma(m, N, T)) {
-        const half_t* fs;
-        int ld;
-        if ((rc = backbone3(m, x, N, T, &fs, &ld, &to, st))) return rc;
-        return head3(m, fs, ld, N * to, poses, st);
+        const int chunk = std::min(N, dma_chunk(m, T));
+        if ((rc = tik_model_reserve(m, chunk, T))) return rc;
+        for (int n0 = 0; n0 < N; n0 += chunk) {
+            const int n = std::min(chunk, N - n0);
+            const half_t* fs;
+            int ld;
+            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &fs, &ld, &to, st))) return rc;
+            if ((rc = head3(m, fs, ld, n * to, poses + (size_t)n0 * to * m->pose_dim, st))) return rc;
+        }
+        return TIK_OK;
     }
+    if ((rc = tik_model_reserve(m, N, T))) return rc;
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
     const int rows = N * to;
     tik::CgemmArgs h{};

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
     // (each with its own L2); give every XCD a contiguous run of tiles, column
@@ -108,23 +108,40 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     int ktotal = a.seg[0].kt * a.seg[0].nblk;
     if (a.nseg > 1) ktotal += a.seg[1].kt * a.seg[1].nblk;
 
-    // K cursor: (segment, tap, block); c0 = block * 64 halves
+    // DMA by buffer_load ... lds: a buffer resource per operand (SGPRs), the
+    // per-lane row part of the byte offset in a VGPR (recomputed only when the
+    // segment or tap changes), the K-block part in the uniform soffset. An
+    // invalid row (temporal zero padding, past M / Nc) gets an offset past
+    // num_records: the hardware returns zeros.
+    constexpr unsigned OOB = DMA_OOB;
+    int kindu[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) kindu[j] = __builtin_amdgcn_readfirstlane(kind[j] == 2 && (wave * NI + j) * 8 < BM ? 0 : kind[j]);
+    const int nwin = a.M / (V * a.tout);   // samples in the batch (rows are (n, t', w))
     int seg = 0, tap = 0, c0 = 0;
-    const unsigned short* base[NI];
+    unsigned voff[NI];
+    i32x4 rsA, rsB;
+    int ldwb = 0, nblkb = 0;   // weight row stride and blocks of the current segment (halves)
     // segment fields by constant index only: a runtime-indexed kernarg struct
     // becomes vector loads + vmcnt(0) waits that would drain the DMA ring
+    auto set_seg = [&]() {
+        const Seg3 sg = (seg == 0) ? a.seg[0] : a.seg[1];
+        rsA = buf_rsrc(sg.src, (unsigned)(nwin * sg.tin * V * sg.ld * 2));
+        rsB = buf_rsrc(sg.w, (unsigned)(a.Nc * sg.ldw * 2));
+        ldwb = sg.ldw; nblkb = sg.nblk;
+    };
     auto set_tap = [&]() {
         const Seg3 sg = (seg == 0) ? a.seg[0] : a.seg[1];
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-            const unsigned short* p = nullptr;
-            if (kind[j] == 0) {
+            unsigned v = OOB;
+            if (kindu[j] == 0) {
                 const int t = sg.stride * at[j] + tap - sg.pad;
-                if (t >= 0 && t < sg.tin) p = sg.src + (((long long)an[j] * sg.tin + t) * V + aw[j]) * sg.ld + 8 * ck[j];
-            } else if (kind[j] == 1) {
-                p = sg.w + (long long)bcol[j] * sg.ldw + tap * sg.nblk * 64 + 8 * ck[j];
+                if (kind[j] == 0 && t >= 0 && t < sg.tin) v = ((((an[j] * sg.tin + t) * V + aw[j]) * sg.ld) + 8 * ck[j]) * 2;
+            } else if (kindu[j] == 1) {
+                v = (kind[j] == 1) ? (bcol[j] * sg.ldw + 8 * ck[j]) * 2 : OOB;
             }
-            base[j] = p;
+            voff[j] = v;
         }
     };
     const int nb_0 = a.seg[0].nblk * 64, nb_1 = a.seg[1].nblk * 64, kt_0 = a.seg[0].kt, kt_1 = a.seg[1].kt;
@@ -132,17 +149,23 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         c0 += 64;
         if (c0 >= (seg == 0 ? nb_0 : nb_1)) {
             c0 = 0;
+            const int seg0 = seg;
             if (++tap >= (seg == 0 ? kt_0 : kt_1)) { tap = 0; ++seg; }
-            if (seg < a.nseg) set_tap();
+            if (seg < a.nseg) {
+                if (seg != seg0) set_seg();
+                set_tap();
+            }
         }
     };
     auto issue = [&](int slot) {
         unsigned char* dst = smem + slot * STAGEB + wave * NI * 1024;
+        const int soA = c0 * 2, soB = (tap * nblkb * 64 + c0) * 2;
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-            const unsigned short* p = base[j] ? base[j] + c0 : a.zeros;
-            if (DBG != 2 && (NIT % NW == 0 || wave * NI + j < NIT))
-                __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+            if (DBG != 2 && (NIT % NW == 0 || wave * NI + j < NIT)) {
+                if (kindu[j] == 1) dma16(rsB, dst + j * 1024, voff[j], soB);
+                else dma16(rsA, dst + j * 1024, voff[j], soA);
+            }
         }
     };
 
@@ -185,6 +208,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
       if (ktotal > 0) {
         // single stage (LDS-bound tiles): DMA of chunk ch+1 waits for compute(ch);
         // a second resident workgroup per CU supplies the overlap
+        set_seg();
         set_tap();
         issue(0);
         advance();
@@ -201,6 +225,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         }
       }
     } else if (ktotal > 0) {
+        set_seg();
         set_tap();
         issue(0);
         advance();

@@ -37,6 +37,30 @@ __device__ __forceinline__ void split4(const f32x4 v, f16x4& h, f16x4& l) {
     }
 }
 
+// ---- buffer_load ... lds (raw buffer, stride 0): offsets at or past
+// num_records read as zeros, which implements every padded / out-of-range row
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ void tik_llvm_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) unsigned* lds, int size,
+                                             int voffset, int soffset, int offset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+__device__ __forceinline__ i32x4 buf_rsrc(const void* p, unsigned bytes) {
+    const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+    i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+    r[1] = __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu));   // stride 0
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+
+// 16 B per lane from rsrc + voff + soff into LDS at dst (wave-uniform base; lane l -> dst + 16 l)
+__device__ __forceinline__ void dma16(const i32x4 r, void* dst, unsigned voff, int soff) {
+    tik_llvm_raw_buffer_load_lds(r, (__attribute__((address_space(3))) unsigned*)dst, 16, (int)voff, soff, 0, 0);
+}
+
+constexpr unsigned DMA_OOB = 0x80000000u;
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

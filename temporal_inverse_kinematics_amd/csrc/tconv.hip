@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
     constexpr int SMEM = RING > CTILE ? RING : CTILE;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int V = a.V, M = a.M, tin = a.tout;
     int r0, n0;
@@ -101,28 +101,47 @@ __global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
     const int G1 = a.nseg > 1 ? a.seg[1].nblk : 0;
     const int NIT = 3 * G0 + G1;
 
+    // buffer_load ... lds: per-segment resources (SGPRs), per-lane row offsets
+    // fixed per segment (VGPRs), the K-block and tap parts in soffset; rows past
+    // the halo / Nc get an offset past num_records and read as zeros
+    constexpr unsigned OOB = DMA_OOB;
+    const Seg3& S0 = a.seg[0];
+    const Seg3& S1 = a.seg[1];
+    const i32x4 rA0 = buf_rsrc(S0.src, (unsigned)(M * S0.ld * 2));
+    const i32x4 rB0 = buf_rsrc(S0.w, (unsigned)(a.Nc * S0.ldw * 2));
+    i32x4 rA1 = rA0, rB1 = rB0;
+    if (a.nseg > 1) {
+        rA1 = buf_rsrc(S1.src, (unsigned)(M * S1.ld * 2));
+        rB1 = buf_rsrc(S1.w, (unsigned)(a.Nc * S1.ldw * 2));
+    }
+    unsigned ha0[NIA], ha1[NIA], wb0[NIB], wb1[NIB];
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+        ha0[j] = a_row[j] >= 0 ? (a_row[j] * S0.ld + 8 * a_ck[j]) * 2 : OOB;
+        ha1[j] = a_row[j] >= 0 ? (a_row[j] * S1.ld + 8 * a_ck[j]) * 2 : OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+        wb0[j] = b_col[j] >= 0 ? (b_col[j] * S0.ldw + 8 * b_ck[j]) * 2 : OOB;
+        wb1[j] = b_col[j] >= 0 ? (b_col[j] * S1.ldw + 8 * b_ck[j]) * 2 : OOB;
+    }
     auto issue_halo = [&](int grp, int slot, int j0, int j1) {
         const bool s1 = grp >= G0;
-        const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
-        const int c0 = 64 * (s1 ? grp - G0 : grp);
+        const int so = 128 * (s1 ? grp - G0 : grp);
         unsigned char* dst = smem + slot * ASLOT + wave * NIA * 1024;
 #pragma unroll
         for (int j = j0; j < j1; ++j) {
-            const unsigned short* p = a.zeros;
-            if (a_row[j] >= 0) p = sg.src + (long long)a_row[j] * sg.ld + c0 + 8 * a_ck[j];
-            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+            if (s1) dma16(rA1, dst + j * 1024, ha1[j], so);
+            else dma16(rA0, dst + j * 1024, ha0[j], so);
         }
     };
     auto issue_w = [&](int grp, int tap, int slot, int j0, int j1) {
         const bool s1 = grp >= G0;
-        const Seg3 sg = s1 ? a.seg[1] : a.seg[0];
-        const int c0 = 64 * (s1 ? grp - G0 : grp);
         unsigned char* dst = smem + 2 * ASLOT + slot * BSLOT + wave * NIB * 1024;
 #pragma unroll
         for (int j = j0; j < j1; ++j) {
-            const unsigned short* p = a.zeros;
-            if (b_col[j] >= 0) p = sg.w + (long long)b_col[j] * sg.ldw + (s1 ? 0 : tap) * sg.nblk * 64 + c0 + 8 * b_ck[j];
-            __builtin_amdgcn_global_load_lds(p, dst + j * 1024, 16, 0, 0);
+            if (s1) dma16(rB1, dst + j * 1024, wb1[j], 128 * (grp - G0));
+            else dma16(rB0, dst + j * 1024, wb0[j], 128 * (tap * S0.nblk + grp));
         }
     };
 

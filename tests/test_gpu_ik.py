@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg"])
+@pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk"])
 def model(request):
     """fp32 MFMA; f16x3 with the size-based choice of GEMM path (register-staged
     fp32 activations + split-K for small batches, split-plane activations with
@@ -25,11 +25,15 @@ def model(request):
     prec, _, path = request.param.partition("-")
     m = synthetic_model(win_size=64, device="cuda", precision=prec)
     if path:
-        os.environ["TIK_GEMM_PATH"] = path
+        # "dmachunk": the DMA path with sub-batches of at most 3 windows (the
+        # 2 GiB-per-tensor split of large batches, exercised at test sizes)
+        env = {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"} if path == "dmachunk" else {"TIK_GEMM_PATH": path}
+        os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created
         finally:
-            del os.environ["TIK_GEMM_PATH"]
+            for k in env:
+                del os.environ[k]
     return m
 
 
@@ -152,3 +156,20 @@ def test_window_gather_vs_reference():
 def test_cpu_tensor_refused(model):
     with pytest.raises(RuntimeError):
         model(torch.zeros(1, 9, 17, 3))
+
+
+def test_model_dma_subbatches_past_2gib(model):
+    """4000 x 64-frame windows: the largest split-block tensor of one call
+    would pass 2 GiB (32-bit buffer offsets), so the DMA path runs two
+    sub-batches; windows on both sides of the split equal their solo solves."""
+    if model.regressor.tik_precision != "f16x3":
+        pytest.skip("the sub-batch split belongs to the f16x3 DMA path")
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    N = 4000
+    x = torch.from_numpy(syn.synthetic_windows(N, 64, seed=5)).cuda()
+    with torch.no_grad():
+        y = model(x)["poses"]
+        pick = [0, 3853, 3854, 3855, 3856, N - 1]
+        solo = torch.cat([model(x[i:i + 1])["poses"] for i in pick])
+    assert torch.isfinite(y).all()
+    assert (y[pick] - solo).abs().max().item() < 2e-5

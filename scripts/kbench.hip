@@ -49,7 +49,7 @@ static float* dev_floats(size_t n, float v) {
 static const char* cfg_name(int c) {
     static const char* n[] = {"T128x128", "T128x64",     "G272x64",     "H64x64",      "T128x128_S3", "T128x128_S4",
                               "T256x128_W8", "T256x64_W8", "T128x64_S4", "G272x128_W8", "G272x64_S2",
-                              "dbg128x128_DMA", "dbg128x128_MFMA", "dbg128x64_DMA", "dbg128x64_MFMA"};
+                              "dbg128x128_DMA", "dbg128x128_MFMA", "dbg128x64_DMA", "dbg128x64_MFMA", "T128x128_W8", "T128x64_W8"};
     return c < tik::C3_NCFG ? n[c] : "?";
 }
 
@@ -197,8 +197,8 @@ int main(int argc, char** argv) {
                    lp / nb / 100.0, ep / nb / 100.0, wl / nb, wv / nb, wb / nb);
         }
         std::vector<int> tc;
-        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T256x128_W8, tik::C3_T128x128_S3, tik::C3_T128x64};
-        else tc = {tik::C3_T128x64, tik::C3_T256x64_W8, tik::C3_T128x64_S4};
+        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T128x128_W8};
+        else tc = {tik::C3_T128x64, tik::C3_T128x64_W8};
         best = 1e9; cur = 0;
         for (int c : tc) {
             const float ms = time_launch(t, c, st, reps);

@@ -253,7 +253,7 @@ struct Layer {
     // f16x3 on split-block activations (cgemm3.hip, DMA-staged). x: SB rows
     // [N*tin*V][ld] halves; z / out: SB rows of 64*ceil(cout/32) halves.
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
-                 bool use_halo = true) const {
+                 bool use_halo = false) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -295,7 +295,7 @@ struct Layer {
         } else {
             const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
-            HIP_TRY(tik::launch_cgemm3(t, big ? tik::C3_T128x128 : tik::C3_T128x64, st));
+            HIP_TRY(tik::launch_cgemm3(t, big ? tik::C3_T128x128_W8 : tik::C3_T128x64_W8, st));
         }
         return TIK_OK;
     }

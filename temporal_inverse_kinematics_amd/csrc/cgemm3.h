@@ -53,7 +53,8 @@ enum Cgemm3Cfg {
     C3_T128x128_S3 = 4, C3_T128x128_S4 = 5, C3_T256x128_W8 = 6, C3_T256x64_W8 = 7, C3_T128x64_S4 = 8,
     C3_G272x128_W8 = 9, C3_G272x64_S2 = 10,
     C3_DBG_T128x128_DMA = 11, C3_DBG_T128x128_MFMA = 12, C3_DBG_T128x64_DMA = 13, C3_DBG_T128x64_MFMA = 14,
-    C3_NCFG = 15,
+    C3_T128x128_W8 = 15, C3_T128x64_W8 = 16,
+    C3_NCFG = 17,
 };
 
 hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st);

@@ -20,16 +20,17 @@
 
 namespace tik {
 
-template <int BN>
-__global__ __launch_bounds__(256) void tconv_halo_kernel(Cgemm3Args a) {
-    constexpr int BM = 128, WM = 2, WN = 2, NT = 256;
+template <int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void tconv_halo_kernel(Cgemm3Args a) {
+    constexpr int BM = 128, NW = WM * WN, NT = 64 * NW;
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
     constexpr int HMAX = 192;             // halo rows in the image (>= 11 frames x 17)
     constexpr int ZR = HMAX - 1;          // a row that is always zero-filled
     constexpr int ASLOT = HMAX * 128;     // split-block rows: 128 B = 32 channels hi | lo
     constexpr int BSLOT = BN * 128;
-    constexpr int NIA = HMAX / 8 / 4;     // halo DMA wave-instructions (8 rows each) per wave
-    constexpr int NIB = BN / 8 / 4;       // weight DMA wave-instructions per wave
+    constexpr int NIA = HMAX / 8 / NW;    // halo DMA wave-instructions (8 rows each) per wave
+    constexpr int NIB = BN / 8 / NW;      // weight DMA wave-instructions per wave
+    static_assert(NIA * 8 * NW == HMAX && NIB * 8 * NW == BN, "DMA split");
     constexpr int LDC = BN + 4;
     constexpr int CTILE = BM * LDC * 4;
     constexpr int RING = 2 * ASLOT + 2 * BSLOT;
@@ -248,9 +249,11 @@ hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st) {
         if (a.seg[s].nblk <= 0 || a.seg[s].ld % 8 || a.seg[s].ld < 64 * a.seg[s].nblk || !a.seg[s].w) return hipErrorInvalidValue;
     if (a.out_h && (a.ldo % 8 || a.ldo < 64 * sb_blocks(a.Nc))) return hipErrorInvalidValue;
     (void)hipGetLastError();
-    const dim3 grid((a.M + 127) / 128, (a.Nc + bn - 1) / bn), blk(256);
-    if (bn == 128) hipLaunchKernelGGL(tconv_halo_kernel<128>, grid, blk, 0, st, a);
-    else hipLaunchKernelGGL(tconv_halo_kernel<64>, grid, blk, 0, st, a);
+    // 8 waves (4 per SIMD with two workgroups per CU) hide the barrier and
+    // LDS latencies of the 1-chunk-in-flight ring better than 4
+    const dim3 grid((a.M + 127) / 128, (a.Nc + bn - 1) / bn), blk(512);
+    if (bn == 128) hipLaunchKernelGGL((tconv_halo_kernel<128, 2, 4>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((tconv_halo_kernel<64, 4, 2>), grid, blk, 0, st, a);
     return hipGetLastError();
 }
 

@@ -270,6 +270,11 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     const unsigned long long tl1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
 
     // ---- epilogues (C tile staged through LDS) -----------------------------
+    // identity residual (EPI_BIAS): loads issued before the C-tile staging so
+    // their latency overlaps it
+    constexpr int KIE = (EPI == EPI_BIAS) ? EpiMap<BM, BN, NT>::KI : 1;
+    f16x4 rh[KIE], rl[KIE];
+    if constexpr (EPI == EPI_BIAS) epi_resid<BM, BN, NT>(a, r0, n0, tid, rh, rl);
     const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
     const int ccol0 = wn * FN * 16 + (lane & 15);
     float* Cs = reinterpret_cast<float*>(smem);
@@ -279,11 +284,13 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         for (int j = 0; j < FN; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
-    __syncthreads();
+    // LDS-only barrier: __syncthreads() would also drain the residual loads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 
     if constexpr (EPI == EPI_BIAS) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_s + 4 * (tid % (BN / 4)));
-        epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid);
+        epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, rh, rl);
     } else {
         // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread;
         // A_eff and the bias come from LDS, the sparse/dense choice is hoisted

@@ -68,34 +68,48 @@ __device__ __forceinline__ void wait_vm() {
 
 // Bias epilogue of a BM x BN fp32 tile staged in LDS (row stride LDC floats):
 // v = act(C + bias + residual) -> SB output and/or fp32. bv = this thread's 4
-// bias values (columns n0 + 4*(tid % (BN/4)) ...), zero past Nc. All residual
-// loads are issued before any store, and the math between stores is
-// branch-free (a data-dependent branch between stores makes the compiler wait
-// for every outstanding store: vmcnt counts stores too).
-template <int BM, int BN, int NT, int LDC>
-__device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, const f32x4 bv, int r0, int n0, int tid) {
-    constexpr int C4 = BN / 4;
+// bias values (columns n0 + 4*(tid % (BN/4)) ...), zero past Nc. The
+// residual is loaded by epi_resid (the caller issues it early, during the
+// last K step, so its latency hides behind the MFMAs); the math between the
+// stores is branch-free (a data-dependent branch between stores makes the
+// compiler wait for every outstanding store: vmcnt counts stores too).
+template <int BM, int BN, int NT>
+struct EpiMap {
+    static constexpr int C4 = BN / 4;
     static_assert(NT % C4 == 0, "epilogue mapping");
-    constexpr int RS = NT / C4;          // rows between one thread's items
-    constexpr int KI = BM / RS;          // items per thread
+    static constexpr int RS = NT / C4;   // rows between one thread's items
+    static constexpr int KI = BM / RS;   // items per thread
+};
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epi_resid(const Cgemm3Args& a, int r0, int n0, int tid, f16x4* rh, f16x4* rl) {
+    using E = EpiMap<BM, BN, NT>;
+    const int c4 = tid % E::C4, lr0 = tid / E::C4;
+    const int col = n0 + 4 * c4;
+#pragma unroll
+    for (int k = 0; k < E::KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
+    if (a.resid && col + 3 < a.Nc) {
+#pragma unroll
+        for (int k = 0; k < E::KI; ++k) {
+            const int row = r0 + lr0 + k * E::RS;
+            if (row < a.M) {
+                const unsigned short* rp = a.resid + (size_t)row * a.ldr + sbc(col);
+                rh[k] = *reinterpret_cast<const f16x4*>(rp);
+                rl[k] = *reinterpret_cast<const f16x4*>(rp + 32);
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int NT, int LDC>
+__device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, const f32x4 bv, int r0, int n0, int tid,
+                                         const f16x4* rh, const f16x4* rl) {
+    using E = EpiMap<BM, BN, NT>;
+    constexpr int C4 = E::C4, RS = E::RS, KI = E::KI;
     const int c4 = tid % C4, lr0 = tid / C4;
     const int col = n0 + 4 * c4;
     const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
     if (col + 3 < a.Nc) {
-        f16x4 rh[KI], rl[KI];
-#pragma unroll
-        for (int k = 0; k < KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
-        if (a.resid) {
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const int row = r0 + lr0 + k * RS;
-                if (row < a.M) {
-                    const unsigned short* rp = a.resid + (size_t)row * a.ldr + sbc(col);
-                    rh[k] = *reinterpret_cast<const f16x4*>(rp);
-                    rl[k] = *reinterpret_cast<const f16x4*>(rp + 32);
-                }
-            }
-        }
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const int lr = lr0 + k * RS, row = r0 + lr;

@@ -49,7 +49,7 @@ static float* dev_floats(size_t n, float v) {
 static const char* cfg_name(int c) {
     static const char* n[] = {"T128x128", "T128x64",     "G272x64",     "H64x64",      "T128x128_S3", "T128x128_S4",
                               "T256x128_W8", "T256x64_W8", "T128x64_S4", "G272x128_W8", "G272x64_S2",
-                              "dbg128x128_DMA", "dbg128x128_MFMA", "dbg128x64_DMA", "dbg128x64_MFMA", "T128x128_W8", "T128x64_W8"};
+                              "dbg128x128_DMA", "dbg128x128_MFMA", "dbg128x64_DMA", "dbg128x64_MFMA", "T128x128_W8", "T128x64_W8", "dbgW8_DMA", "dbgW8_MFMA"};
     return c < tik::C3_NCFG ? n[c] : "?";
 }
 
@@ -196,19 +196,38 @@ int main(int argc, char** argv) {
             printf("  trace halo                                  loop %6.2f us  epilogue %6.2f us                  | wave0 loop %6.0f clk vm-wait %6.0f barrier %6.0f\n",
                    lp / nb / 100.0, ep / nb / 100.0, wl / nb, wv / nb, wb / nb);
         }
+        {
+            const int tg[] = {tik::TG_128x128, tik::TG_128x64, tik::TG_128x128_A4, tik::TG_128x64_A4};
+            const char* tn[] = {"TG_128x128", "TG_128x64", "TG_128x128_A4", "TG_128x64_A4"};
+            for (int q = 0; q < 4; ++q) {
+                if (Ly.cout < 128 && (q == 0 || q == 2)) continue;
+                hipEvent_t e0, e1;
+                CK(hipEventCreate(&e0));
+                CK(hipEventCreate(&e1));
+                for (int i = 0; i < 3; ++i) CK(tik::launch_tgemm(t, tg[q], st));
+                CK(hipEventRecord(e0, st));
+                for (int i = 0; i < reps; ++i) CK(tik::launch_tgemm(t, tg[q], st));
+                CK(hipEventRecord(e1, st));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                printf("L%d T %-12s %8.4f ms  %6.1f TF(fp32-eq)\n", l, tn[q], ms / reps,
+                       2.0 * rout * Ly.cout * (3.0 * Ly.cout + (t.nseg > 1 ? Ly.cin : 0)) / (ms / reps) / 1e9);
+            }
+        }
         std::vector<int> tc;
-        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T128x128_W8};
+        if (Ly.cout >= 128) tc = {tik::C3_T128x128, tik::C3_T128x128_W8, tik::C3_DBG_W8_DMA, tik::C3_DBG_W8_MFMA};
         else tc = {tik::C3_T128x64, tik::C3_T128x64_W8};
         best = 1e9; cur = 0;
         for (int c : tc) {
             const float ms = time_launch(t, c, st, reps);
             if (c == tc[0]) cur = ms;
-            if (ms < best && c < tik::C3_DBG_T128x128_DMA) best = ms;
+            if (ms < best && (c < tik::C3_DBG_T128x128_DMA || c > tik::C3_DBG_T128x64_MFMA) && c < tik::C3_DBG_W8_DMA) best = ms;
             printf("L%d T %-12s %8.4f ms  %6.1f TF(fp32-eq)\n", l, cfg_name(c), ms, tfl / ms / 1e9);
         }
         tot_best += best; tot_cur += cur;
         {
-            const int cfgT = Ly.cout >= 128 ? tik::C3_T128x128 : tik::C3_T128x64;
+            const int cfgT = Ly.cout >= 128 ? tik::C3_T128x128_W8 : tik::C3_T128x64_W8;
             const int nb = (int)((rout + 127) / 128) * (Ly.cout >= 128 ? (Ly.cout + 127) / 128 : (Ly.cout + 63) / 64);
             t.tune = 0;
             trace_launch(cfg_name(cfgT), t, cfgT, st, nb);

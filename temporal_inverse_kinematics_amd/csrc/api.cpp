@@ -295,7 +295,7 @@ struct Layer {
         } else {
             const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
-            HIP_TRY(tik::launch_cgemm3(t, big ? tik::C3_T128x128_W8 : tik::C3_T128x64_W8, st));
+            HIP_TRY(tik::launch_tgemm(t, big ? tik::TG_128x128 : tik::TG_128x64, st));
         }
         return TIK_OK;
     }

@@ -53,11 +53,21 @@ enum Cgemm3Cfg {
     C3_T128x128_S3 = 4, C3_T128x128_S4 = 5, C3_T256x128_W8 = 6, C3_T256x64_W8 = 7, C3_T128x64_S4 = 8,
     C3_G272x128_W8 = 9, C3_G272x64_S2 = 10,
     C3_DBG_T128x128_DMA = 11, C3_DBG_T128x128_MFMA = 12, C3_DBG_T128x64_DMA = 13, C3_DBG_T128x64_MFMA = 14,
-    C3_T128x128_W8 = 15, C3_T128x64_W8 = 16,
-    C3_NCFG = 17,
+    C3_T128x128_W8 = 15, C3_T128x64_W8 = 16, C3_DBG_W8_DMA = 17, C3_DBG_W8_MFMA = 18,
+    C3_NCFG = 19,
 };
 
 hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st);
+
+// bias-epilogue GEMM with split DMA rings (tgemm.hip): A ring NSA deep, B ring 2
+enum TgemmCfg {
+    TG_128x128 = 0,      // 8 waves, A ring 3
+    TG_128x64 = 1,       // 8 waves, A ring 3
+    TG_128x128_A4 = 2,   // A ring 4 (one workgroup per CU)
+    TG_128x64_A4 = 3,
+    TG_64x64 = 4,        // head Linear layers, 4 waves
+};
+hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st);
 
 // stride-1 temporal conv + residual with a frame halo in LDS (tconv.hip):
 // seg[0] kt=3/stride 1/pad 1, optional seg[1] kt=1 (residual conv), V=17,

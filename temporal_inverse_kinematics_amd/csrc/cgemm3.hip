@@ -389,6 +389,8 @@ hipError_t launch_cgemm3(const Cgemm3Args& a, int cfg, hipStream_t st) {
         case C3_DBG_T128x64_MFMA: return launch3<128, 64, 2, 2, EPI_BIAS, 0, 3, 2>(a, st);
         case C3_T128x128_W8: return launch3<128, 128, 2, 4, EPI_BIAS, 0, 2>(a, st);
         case C3_T128x64_W8: return launch3<128, 64, 4, 2, EPI_BIAS, 0, 3>(a, st);
+        case C3_DBG_W8_DMA: return launch3<128, 128, 2, 4, EPI_BIAS, 0, 2, 1>(a, st);
+        case C3_DBG_W8_MFMA: return launch3<128, 128, 2, 4, EPI_BIAS, 0, 2, 2>(a, st);
         case C3_G272x64_S2:
             if (a.V != 17) return hipErrorInvalidValue;
             return launch3<272, 64, 1, 4, EPI_GRAPH, 17, 2>(a, st);

@@ -1,0 +1,247 @@
+// tgemm.hip — the bias-epilogue f16x3 implicit GEMM (temporal conv +
+// residual, head Linear) with SPLIT DMA rings: the activation operand A
+// (first-touch rows, HBM/MALL latency) is fetched NSA-1 K steps ahead, the
+// weight operand B (L2-resident, short latency) one step ahead.
+//
+// cgemm3.hip keeps one stage (A and B together) in flight per workgroup;
+// its K loop was measured to be bound by that single ~2 µs DMA round trip
+// (DMA-only runs took 87 % of the full kernel time). With a 3-deep A ring and
+// a 2-deep B ring, 48 KB per workgroup (96 KB per CU) stay in flight and the
+// critical A rows get two K steps of lead, in the same 80 KB of LDS that lets
+// two workgroups share a CU.
+//
+// Issue order per K step is B(ch+1) then A(ch+2), so the counted wait at step
+// ch — vmcnt(NIA_w) — retires A(ch) and B(ch) and leaves only A(ch+1) in
+// flight (vmcnt retires in issue order).
+#include "cgemm3_dev.h"
+
+namespace tik {
+
+template <int BM, int BN, int WM, int WN, int NSA>
+__global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
+    constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+    constexpr int NW = WM * WN, NT = 64 * NW;
+    static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN, "tile");
+    constexpr int NIA = BM / 8 / NW, NIB = BN / 8 / NW;   // DMA instructions per wave per stage
+    static_assert(NIA * 8 * NW == BM && NIB * 8 * NW == BN, "DMA split");
+    constexpr int NSB = 2;
+    constexpr int ASLOT = BM * 128, BSLOT = BN * 128;
+    constexpr int RING = NSA * ASLOT + NSB * BSLOT;
+    constexpr int LDC = BN + 4;
+    constexpr int CTILE = BM * LDC * 4;
+    constexpr int SMEM = RING > CTILE ? RING : CTILE;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];   // the only LDS object
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    int r0, n0;
+    {   // XCD-aware tile order (cgemm3.hip)
+        const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+        const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
+        const int swz = (a.tune & 1) ? bid : x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        r0 = (swz / gridDim.y) * BM;
+        n0 = (swz % gridDim.y) * BN;
+    }
+    const int V = a.V;
+    const unsigned long long ts0 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // ---- DMA roles. A instruction j of this wave: A image rows (wave*NIA+j)*8 ..+7;
+    // B instruction j: B image rows (wave*NIB+j)*8 ..+7; lane l writes unit l&7 of row l>>3.
+    int a_n[NIA], a_t[NIA], a_w[NIA], a_ck[NIA];
+    bool a_ok[NIA];
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+        const int rr = (wave * NIA + j) * 8 + (lane >> 3);
+        const int row = r0 + rr;
+        a_ck[j] = (lane & 7) ^ sbf(rr);
+        a_ok[j] = row < a.M;
+        const int q = a_ok[j] ? row / V : 0;
+        a_w[j] = a_ok[j] ? row - q * V : 0;
+        a_n[j] = q / a.tout;
+        a_t[j] = q - a_n[j] * a.tout;
+    }
+    int b_col[NIB], b_ck[NIB];
+#pragma unroll
+    for (int j = 0; j < NIB; ++j) {
+        const int rr = (wave * NIB + j) * 8 + (lane >> 3);
+        b_ck[j] = (lane & 7) ^ sbf(rr);
+        b_col[j] = n0 + rr < a.Nc ? n0 + rr : -1;
+    }
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    {
+        const int col = n0 + 4 * (tid % (BN / 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (a.bias && col + e < a.Nc) bv[e] = a.bias[col + e];
+    }
+
+    const int ktotal = a.seg[0].kt * a.seg[0].nblk + (a.nseg > 1 ? a.seg[1].kt * a.seg[1].nblk : 0);
+    const int nwin = a.M / (V * a.tout);
+
+    // Two independent K cursors (A runs one step ahead of B). Each keeps its
+    // own (segment, tap, block) and its own per-lane offsets.
+    struct Cur { int seg, tap, blk; };
+    auto step = [&](Cur& c) {
+        const int nb = c.seg == 0 ? a.seg[0].nblk : a.seg[1].nblk;
+        const int kt = c.seg == 0 ? a.seg[0].kt : a.seg[1].kt;
+        if (++c.blk >= nb) { c.blk = 0; if (++c.tap >= kt) { c.tap = 0; ++c.seg; } }
+    };
+    Cur ca{0, 0, 0}, cb{0, 0, 0};
+    unsigned a_off[NIA], b_off[NIB];
+    i32x4 rA = buf_rsrc(a.seg[0].src, (unsigned)(nwin * a.seg[0].tin * V * a.seg[0].ld * 2));
+    i32x4 rB = buf_rsrc(a.seg[0].w, (unsigned)(a.Nc * a.seg[0].ldw * 2));
+    int a_seg_cached = -1, a_tap_cached = -1, b_seg_cached = -1;
+    auto a_prepare = [&]() {   // per-lane A offsets for cursor ca's (segment, tap)
+        if (ca.seg == a_seg_cached && ca.tap == a_tap_cached) return;
+        const Seg3 sg = ca.seg == 0 ? a.seg[0] : a.seg[1];
+        if (ca.seg != a_seg_cached) rA = buf_rsrc(sg.src, (unsigned)(nwin * sg.tin * V * sg.ld * 2));
+#pragma unroll
+        for (int j = 0; j < NIA; ++j) {
+            const int t = sg.stride * a_t[j] + ca.tap - sg.pad;
+            a_off[j] = (a_ok[j] && t >= 0 && t < sg.tin)
+                           ? (unsigned)((((a_n[j] * sg.tin + t) * V + a_w[j]) * sg.ld + 8 * a_ck[j]) * 2)
+                           : DMA_OOB;
+        }
+        a_seg_cached = ca.seg; a_tap_cached = ca.tap;
+    };
+    auto b_prepare = [&]() {
+        if (cb.seg == b_seg_cached) return;
+        const Seg3 sg = cb.seg == 0 ? a.seg[0] : a.seg[1];
+        rB = buf_rsrc(sg.w, (unsigned)(a.Nc * sg.ldw * 2));
+#pragma unroll
+        for (int j = 0; j < NIB; ++j)
+            b_off[j] = b_col[j] >= 0 ? (unsigned)((b_col[j] * sg.ldw + 8 * b_ck[j]) * 2) : DMA_OOB;
+        b_seg_cached = cb.seg;
+    };
+    auto issue_a = [&](int slot) {   // A stage of cursor ca, then advance it
+        a_prepare();
+        unsigned char* dst = smem + slot * ASLOT + wave * NIA * 1024;
+#pragma unroll
+        for (int j = 0; j < NIA; ++j) dma16(rA, dst + j * 1024, a_off[j], ca.blk * 128);
+        step(ca);
+    };
+    auto issue_b = [&](int slot) {
+        b_prepare();
+        const int nb = cb.seg == 0 ? a.seg[0].nblk : a.seg[1].nblk;
+        unsigned char* dst = smem + NSA * ASLOT + slot * BSLOT + wave * NIB * 1024;
+#pragma unroll
+        for (int j = 0; j < NIB; ++j) dma16(rB, dst + j * 1024, b_off[j], (cb.tap * nb + cb.blk) * 128);
+        step(cb);
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int arow = wm * FM * 16 + (lane & 15);
+    const int brow = wn * FN * 16 + (lane & 15);
+    const int g = lane >> 4;
+    auto compute = [&](int as, int bs) {
+        const unsigned char* A = smem + as * ASLOT;
+        const unsigned char* B = smem + NSA * ASLOT + bs * BSLOT;
+        f16x8 bh[FN], bl[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            bh[j] = *reinterpret_cast<const f16x8*>(B + sbo(brow + j * 16, g));
+            bl[j] = *reinterpret_cast<const f16x8*>(B + sbo(brow + j * 16, 4 + g));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(A + sbo(arow + i * 16, g));
+            const f16x8 al = *reinterpret_cast<const f16x8*>(A + sbo(arow + i * 16, 4 + g));
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+
+    unsigned long long tw_vm = 0, tw_bar = 0;
+    const unsigned long long tl0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+    if (ktotal > 0) {
+        // prologue: B(0); A(0) .. A(NSA-2)
+        issue_b(0);
+#pragma unroll
+        for (int s = 0; s < NSA - 1; ++s)
+            if (s < ktotal) issue_a(s);
+        for (int ch = 0; ch < ktotal; ++ch) {
+            const unsigned long long w0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+            // in flight (issue order): A(ch) .. | B(ch) | A(ch+1) .. A(ch+NSA-2):
+            // retire everything up to B(ch), leave the younger A stages
+            const int younger = min(NSA - 2, ktotal - 1 - ch);
+            if (NSA >= 3 && younger >= 1) wait_vm<(NSA >= 3 ? NIA : 0)>();
+            else wait_vm<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const unsigned long long w1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+            __builtin_amdgcn_s_barrier();
+            if (a.trace) {
+                const unsigned long long w2 = __builtin_amdgcn_s_memtime();
+                tw_vm += w1 - w0; tw_bar += w2 - w1;
+            }
+            if (ch + 1 < ktotal) issue_b((ch + 1) % NSB);
+            if (ch + NSA - 1 < ktotal) issue_a((ch + NSA - 1) % NSA);
+            compute(ch % NSA, ch % NSB);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long ts1 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long tl1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
+
+    f16x4 rh[EpiMap<BM, BN, NT>::KI], rl[EpiMap<BM, BN, NT>::KI];
+    epi_resid<BM, BN, NT>(a, r0, n0, tid, rh, rl);
+    const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
+    const int ccol0 = wn * FN * 16 + (lane & 15);
+    float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, rh, rl);
+
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long* t = a.trace + 5 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+            t[0] = ts0; t[1] = ts1; t[2] = __builtin_amdgcn_s_memrealtime();
+            t[3] = tw_vm;
+            t[4] = tw_bar | ((unsigned long long)(tl1 - tl0) << 32);
+        }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int NSA>
+static hipError_t launch_t(const Cgemm3Args& a, hipStream_t st) {
+    const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN), blk(64 * WM * WN);
+    hipLaunchKernelGGL((tgemm_kernel<BM, BN, WM, WN, NSA>), g, blk, 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st) {
+    if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
+    for (int s = 0; s < a.nseg; ++s)
+        if (a.seg[s].nblk <= 0 || a.seg[s].ld % 8 || a.seg[s].ld < 64 * a.seg[s].nblk || !a.seg[s].w ||
+            a.seg[s].ldw < a.seg[s].kt * a.seg[s].nblk * 64)
+            return hipErrorInvalidValue;
+    if (a.out_h && (a.ldo % 8 || a.ldo < 64 * sb_blocks(a.Nc))) return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    switch (cfg) {
+        case TG_128x128: return launch_t<128, 128, 2, 4, 3>(a, st);
+        case TG_128x64: return launch_t<128, 64, 4, 2, 3>(a, st);
+        case TG_128x128_A4: return launch_t<128, 128, 2, 4, 4>(a, st);
+        case TG_128x64_A4: return launch_t<128, 64, 4, 2, 4>(a, st);
+        case TG_64x64: return launch_t<64, 64, 2, 2, 3>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace tik

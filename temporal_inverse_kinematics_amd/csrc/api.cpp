@@ -131,6 +131,7 @@ struct Layer {
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
     SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3, register-staged path)
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
+    DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -186,6 +187,12 @@ struct Layer {
             }
             if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)))
                 return rc;
+            if (cin <= 4) {
+                std::vector<float> h0((size_t)cout * cin);
+                for (int co = 0; co < cout; ++co)
+                    for (int ci = 0; ci < cin; ++ci) h0[(size_t)co * cin + ci] = hwr[(size_t)co * cinp + ci];
+                if ((rc = wr0.upload(h0))) return rc;
+            }
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
         mix_sparse = tik::fits_coco_hop2(ha.data(), V);
@@ -252,8 +259,17 @@ struct Layer {
 
     // f16x3 on split-block activations (cgemm3.hip, DMA-staged). x: SB rows
     // [N*tin*V][ld] halves; z / out: SB rows of 64*ceil(cout/32) halves.
+    // Raw-input first layer (cin <= 4, residual conv, stride 1): the data_bn'd
+    // keypoints feed the gcn (layer0.hip) and the residual conv (tcn epilogue)
+    // directly, no split-block input.
+    bool raw_ok() const {
+        return index == 0 && cin <= 4 && res == RES_CONV && stride == 1 && wr0.p && cout >= 16 && cout % 4 == 0 &&
+               256 % (cout / 4) == 0;
+    }
+
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
-                 bool use_halo = false) const {
+                 bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
+                 const float* bn_sh = nullptr, float* xb4 = nullptr) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -264,7 +280,12 @@ struct Layer {
         g.bias = bias2.p; g.out_h = z; g.ldo = ldz; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
         const double px_in = (double)rin, px_out = (double)rout;
-        {
+        if (xraw) {
+            ProfScope p("G0_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                        4.0 * (px_in * cin + px_in * cout), st);
+            HIP_TRY(tik::launch_gcn0(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
+                                     cout, z, ldz, xb4, st));
+        } else {
             // 128-column tiles (8 waves) read each input row once per 128 outputs
             const bool wide = cout % 128 == 0;
             const std::string lab = std::string(wide ? "G3_272x128.L" : "G3_272x64.L") + std::to_string(index);
@@ -276,7 +297,9 @@ struct Layer {
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
         t.seg[0] = mkseg3(z, ldz, sbt, TK, stride, 1, tin);
         t.nseg = 1;
-        if (res == RES_CONV) {
+        if (xraw) {
+            t.rx = xb4; t.rxc = cin; t.rw = wr0.p;
+        } else if (res == RES_CONV) {
             t.seg[1] = mkseg3(x, ld, sbr, 1, stride, 0, tin);
             t.nseg = 2;
         } else if (res == RES_IDEN) {
@@ -502,7 +525,7 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
     const int V = m->V;
     half_t* xs = reinterpret_cast<half_t*>(m->xb.p);
     const long long px = (long long)N * T * V;
-    {
+    if (!(m->layers.front().raw_ok() && m->layers.front().cin == m->C0)) {
         ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
         HIP_TRY(tik::launch_data_bn_split(x, (int)px, V, m->C0, m->bn_sc.p, m->bn_sh.p, xs, st));
     }
@@ -512,7 +535,10 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
     int which = 0;
     for (const Layer& L : m->layers) {
         half_t* o = bufs[which];
-        if ((rc = L.forward3(cur, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st))) return rc;
+        const bool raw = &L == &m->layers.front() && L.raw_ok() && L.cin == m->C0;
+        if ((rc = L.forward3(cur, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st, false,
+                             raw ? x : nullptr, m->bn_sc.p, m->bn_sh.p, m->xb.p)))
+            return rc;
         t = Layer::tout(t, L.stride);
         cur = o; ld = 64 * L.sbt.nblk; which ^= 1;
     }

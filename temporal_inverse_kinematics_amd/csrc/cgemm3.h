@@ -36,6 +36,11 @@ struct Cgemm3Args {
     int ldo;
     float* out_f;                 // fp32 output [M][ldf] (or null)
     int ldf;
+    // small residual conv on a 4-float-per-row input (layer 0, EPI_BIAS):
+    // res[r][c] = sum_{k < rxc} rx[r][k] * rw[c][k]; rx [M][4] fp32 (data_bn applied), rxc <= 4
+    const float* rx;
+    int rxc;
+    const float* rw;
     const float* amix;            // EPI_GRAPH [V][V]
     int act;
     int mix_sparse;
@@ -74,6 +79,13 @@ hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st);
 // Nc % 64 == 0; bn = 64 or 128 output columns per tile
 bool tconv_halo_ok(const Cgemm3Args& a);
 hipError_t launch_tconv_halo(const Cgemm3Args& a, int bn, hipStream_t st);
+
+// layer 0 spatial half straight from the raw keypoints (layer0.hip):
+// z = ReLU(mix_A(data_bn(x) . Wg'^T) + bias2) -> SB [rows][ldo]; x [rows][C0], C0 <= 4;
+// also writes xb4 = data_bn(x) as [rows][4] fp32 (the residual conv's input)
+hipError_t launch_gcn0(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,
+                       const float* wg, int ldwg, const float* bias2, const float* amix, int mix_sparse, int Cout,
+                       unsigned short* out, int ldo, float* xb4, hipStream_t st);
 
 // SB activations [rows][ld] -> fp32 [rows][C]
 hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st);

@@ -273,8 +273,8 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     // identity residual (EPI_BIAS): loads issued before the C-tile staging so
     // their latency overlaps it
     constexpr int KIE = (EPI == EPI_BIAS) ? EpiMap<BM, BN, NT>::KI : 1;
-    f16x4 rh[KIE], rl[KIE];
-    if constexpr (EPI == EPI_BIAS) epi_resid<BM, BN, NT>(a, r0, n0, tid, rh, rl);
+    f32x4 res[KIE];
+    if constexpr (EPI == EPI_BIAS) epi_resid<BM, BN, NT>(a, r0, n0, tid, res);
     const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
     const int ccol0 = wn * FN * 16 + (lane & 15);
     float* Cs = reinterpret_cast<float*>(smem);
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
 
     if constexpr (EPI == EPI_BIAS) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(bias_s + 4 * (tid % (BN / 4)));
-        epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, rh, rl);
+        epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, res);
     } else {
         // graph epilogue: frame-aligned tile; (frame, 4 channels) per thread;
         // A_eff and the bias come from LDS, the sparse/dense choice is hoisted

@@ -10,6 +10,7 @@
 namespace tik {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
@@ -81,43 +82,66 @@ struct EpiMap {
     static constexpr int KI = BM / RS;   // items per thread
 };
 
+// Residual operand of the EPI_BIAS epilogue, loaded before the C-tile staging
+// and consumed after it: the loads stay in flight across the staging (no
+// conversion here — converting would force a vmcnt wait before the barrier).
+// rr[k] holds the raw 16 bytes of item k: the identity residual's SB hi (dwords
+// 0-1) and lo (dwords 2-3) halves, or one [M][4] fp32 row of a.rx.
 template <int BM, int BN, int NT>
-__device__ __forceinline__ void epi_resid(const Cgemm3Args& a, int r0, int n0, int tid, f16x4* rh, f16x4* rl) {
+__device__ __forceinline__ void epi_resid(const Cgemm3Args& a, int r0, int n0, int tid, f32x4* rr) {
     using E = EpiMap<BM, BN, NT>;
     const int c4 = tid % E::C4, lr0 = tid / E::C4;
     const int col = n0 + 4 * c4;
 #pragma unroll
-    for (int k = 0; k < E::KI; ++k) { rh[k] = f16x4{}; rl[k] = f16x4{}; }
-    if (a.resid && col + 3 < a.Nc) {
+    for (int k = 0; k < E::KI; ++k) rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (col + 3 >= a.Nc) return;
+    if (a.resid) {   // identity residual: SB hi + lo
 #pragma unroll
         for (int k = 0; k < E::KI; ++k) {
             const int row = r0 + lr0 + k * E::RS;
             if (row < a.M) {
                 const unsigned short* rp = a.resid + (size_t)row * a.ldr + sbc(col);
-                rh[k] = *reinterpret_cast<const f16x4*>(rp);
-                rl[k] = *reinterpret_cast<const f16x4*>(rp + 32);
+                const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
+                const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
+                rr[k] = f32x4{h[0], h[1], l[0], l[1]};
             }
+        }
+    } else if (a.rx) {   // small residual conv input: [M][4] fp32 rows
+#pragma unroll
+        for (int k = 0; k < E::KI; ++k) {
+            const int row = r0 + lr0 + k * E::RS;
+            if (row < a.M) rr[k] = *reinterpret_cast<const f32x4*>(a.rx + (size_t)row * 4);
         }
     }
 }
 
 template <int BM, int BN, int NT, int LDC>
 __device__ __forceinline__ void epi_bias(const Cgemm3Args& a, const float* Cs, const f32x4 bv, int r0, int n0, int tid,
-                                         const f16x4* rh, const f16x4* rl) {
+                                         const f32x4* rr) {
     using E = EpiMap<BM, BN, NT>;
     constexpr int C4 = E::C4, RS = E::RS, KI = E::KI;
     const int c4 = tid % C4, lr0 = tid / C4;
     const int col = n0 + 4 * c4;
     const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
     if (col + 3 < a.Nc) {
+        // residual-conv weights (a.rx mode; identity mode: w = 0 and rr read as SB halves)
+        const bool conv = a.resid == nullptr && a.rx != nullptr;
+        float w[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w[e][c] = conv && c < a.rxc ? a.rw[(col + e) * a.rxc + c] : 0.f;
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
             const int lr = lr0 + k * RS, row = r0 + lr;
             if (row >= a.M) continue;
             f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + 4 * c4) + bv;
+            const f16x4 h = __builtin_bit_cast(f16x4, f32x2{rr[k][0], rr[k][1]});
+            const f16x4 l = __builtin_bit_cast(f16x4, f32x2{rr[k][2], rr[k][3]});
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                v[e] += (float)rh[k][e] + (float)rl[k][e];
+                v[e] += conv ? rr[k][0] * w[e][0] + rr[k][1] * w[e][1] + rr[k][2] * w[e][2] + rr[k][3] * w[e][3]
+                             : (float)h[e] + (float)l[e];
                 v[e] = v[e] > 0.f ? v[e] : slope * v[e];
             }
             if (a.out_h) {

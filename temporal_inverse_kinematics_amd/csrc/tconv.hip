@@ -218,9 +218,9 @@ __global__ __launch_bounds__(64 * WM * WN) void tconv_halo_kernel(Cgemm3Args a) 
 #pragma unroll
             for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
     __syncthreads();
-    f16x4 rh[EpiMap<BM, BN, NT>::KI], rl[EpiMap<BM, BN, NT>::KI];
-    epi_resid<BM, BN, NT>(a, r0, n0, tid, rh, rl);
-    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, rh, rl);
+    f32x4 res[EpiMap<BM, BN, NT>::KI];
+    epi_resid<BM, BN, NT>(a, r0, n0, tid, res);
+    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, res);
 
     if (a.trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -192,8 +192,8 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
     const unsigned long long ts1 = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const unsigned long long tl1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
 
-    f16x4 rh[EpiMap<BM, BN, NT>::KI], rl[EpiMap<BM, BN, NT>::KI];
-    epi_resid<BM, BN, NT>(a, r0, n0, tid, rh, rl);
+    f32x4 res[EpiMap<BM, BN, NT>::KI];
+    epi_resid<BM, BN, NT>(a, r0, n0, tid, res);
     const int crow0 = wm * FM * 16 + 4 * (lane >> 4);
     const int ccol0 = wn * FN * 16 + (lane & 15);
     float* Cs = reinterpret_cast<float*>(smem);
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
             for (int e = 0; e < 4; ++e) Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = acc[i][j][e];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, rh, rl);
+    epi_bias<BM, BN, NT, LDC>(a, Cs, bv, r0, n0, tid, res);
 
     if (a.trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

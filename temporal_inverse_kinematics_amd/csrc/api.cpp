@@ -10,6 +10,7 @@
 //   poses = (LeakyReLU(feat . W0^T + b0)) . W3^T + b3      pose_trainer.py:89-92
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -269,7 +270,7 @@ struct Layer {
 
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
                  bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
-                 const float* bn_sh = nullptr, float* xb4 = nullptr) const {
+                 const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -280,6 +281,43 @@ struct Layer {
         g.bias = bias2.p; g.out_h = z; g.ldo = ldz; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
         const double px_in = (double)rin, px_out = (double)rout;
+        if (!xraw && stride == 1 && res == RES_IDEN && V == 17 && tik::stblock_ok(cin, cout) && fuse) {
+            // whole block in one kernel: z stays in LDS (stblock.hip)
+            tik::StbArgs b{};
+            b.x = x; b.ldx = ld; b.nwin = N; b.T = tin;
+            b.wg = sbg.w.p; b.ldwg = sbg.ldw; b.bias2 = bias2.p; b.amix = amix.p; b.mix_sparse = mix_sparse ? 1 : 0;
+            b.wt = sbt.w.p; b.ldwt = sbt.ldw; b.bias = biasT.p; b.resid = 1; b.out = out; b.ldo = ldz;
+            const std::string lab = std::string("B3_") + std::to_string(cout) + ".L" + std::to_string(index);
+            ProfScope p(lab.c_str(),
+                        2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * TK * cout * cout,
+                        4.0 * (px_in * cin + px_out * cout + (double)cout * cin + (double)TK * cout * cout), st);
+            static const bool trace = getenv("TIK_STB_TRACE") != nullptr;
+            if (!trace) {
+                HIP_TRY(tik::launch_stblock(b, cin, cout, st));
+                return TIK_OK;
+            }
+            // debug hook: per-phase workgroup timing (G, y store, mix, T, epilogue), printed to stderr
+            const int F = 14;
+            const int nwg = (N * tin + F - 1) / F;
+            unsigned long long* d = nullptr;
+            HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
+            b.trace = d;
+            HIP_TRY(tik::launch_stblock(b, cin, cout, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            std::vector<unsigned long long> h((size_t)nwg * 6);
+            HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(hipFree(d));
+            double ph[5] = {0, 0, 0, 0, 0};
+            unsigned long long lo = ~0ull, hi = 0;
+            for (int w = 0; w < nwg; ++w) {
+                for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
+                lo = std::min(lo, h[6 * w]); hi = std::max(hi, h[6 * w + 5]);
+            }
+            fprintf(stderr, "stblock L%d (%d wg): per-wg us G %.2f wt-issue %.2f mix %.2f T %.2f epi %.2f | span %.1f us\n",
+                    index, nwg, ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100,
+                    ph[4] / nwg / 100, (hi - lo) / 100.0);
+            return TIK_OK;
+        }
         if (xraw) {
             ProfScope p("G0_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout), st);
@@ -340,6 +378,7 @@ struct tik_model {
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
     int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
+    bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
     Profiler prof;
     bool profiling = false;
 };
@@ -430,6 +469,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         return rc;
     }
     if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
+    if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
         else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
@@ -537,7 +577,7 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
         half_t* o = bufs[which];
         const bool raw = &L == &m->layers.front() && L.raw_ok() && L.cin == m->C0;
         if ((rc = L.forward3(cur, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st, false,
-                             raw ? x : nullptr, m->bn_sc.p, m->bn_sh.p, m->xb.p)))
+                             raw ? x : nullptr, m->bn_sc.p, m->bn_sh.p, m->xb.p, m->stblock)))
             return rc;
         t = Layer::tout(t, L.stride);
         cur = o; ld = 64 * L.sbt.nblk; which ^= 1;

@@ -88,6 +88,29 @@ hipError_t launch_gcn0(const float* x, int rows, int V, int C0, const float* bn_
                        unsigned short* out, int ldo, float* xb4, hipStream_t st);
 
 // SB activations [rows][ld] -> fp32 [rows][C]
+// One whole stride-1, identity-residual ST-GCN block per workgroup
+// (stblock.hip): z = ReLU(mix(x Wg') + bias2) stays in LDS, then
+// out = ReLU(tcn(z) + bias + x). x / out: SB rows (n, t, v) of nwin windows x T frames.
+struct StbArgs {
+    const unsigned short* x;
+    int ldx;
+    int nwin, T;
+    const unsigned short* wg;   // SB [Cout][Cin/32][64]
+    int ldwg;
+    const float* bias2;         // [17][Cout]
+    const float* amix;          // [17][17], input joint v -> output joint w at v*17+w
+    int mix_sparse;
+    const unsigned short* wt;   // SB [Cout][3][Cout/32][64]
+    int ldwt;
+    const float* bias;          // [Cout]
+    int resid;                  // 1: + x (identity residual)
+    unsigned short* out;
+    int ldo;
+    unsigned long long* trace;  // optional: 6 s_memrealtime stamps per workgroup (phase boundaries)
+};
+bool stblock_ok(int cin, int cout);
+hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st);
+
 hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st);
 // data_bn on load, straight to one SB block per pixel (C <= 32 channels, rest zero) (st_gcn_aaai18.py:119-125)
 hipError_t launch_data_bn_split(const float* x, int n_px, int V, int C, const float* scale, const float* shift,

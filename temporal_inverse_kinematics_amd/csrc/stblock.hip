@@ -1,0 +1,356 @@
+// stblock.hip — one whole ST-GCN block per workgroup, for the stride-1
+// identity-residual 64-channel blocks (st_gcn_aaai18.py st_gcn.forward:
+// gcn -> tcn -> + x -> ReLU; models.py StbBlock): the spatial half's output
+// z never leaves the CU.
+//
+// The layered path runs a block as two kernels, G (x -> z) and T
+// (z, x -> out): five activation streams through HBM per block (read x,
+// write z, read z, read x, write out). Here one workgroup owns F = 14
+// consecutive output frames (all 64 channels) and
+//   1. G: streams x for the 16 input frames (one halo frame each side, the
+//      temporal taps) and Wg through LDS-DMA. The x image is JOINT-MAJOR
+//      (image row 16 v + f = joint v of frame f), and y = x Wg' is computed
+//      transposed (MFMA A = Wg rows, B = pixel rows): pixel block j is joint
+//      j of the 16 frames, so each lane of waves 0-3 ends holding y for one
+//      frame (lane & 15), 4 channels and ALL 17 joints;
+//   2. mix in registers: z = ReLU(mix_A(y) + bias2) per lane (17x17, fp32,
+//      the COCO 2-hop sparsity unrolled), written once, split, into the
+//      frame-major z image (row 17 f + w) — no y pass through LDS;
+//   3. T: the 3-tap temporal conv with A read straight from the resident z
+//      image (tap k of output row m is z row m + 17 k, or the zero row when
+//      the tap leaves the window) and Wt streamed through the ring;
+//   4. epilogue: C tile staged over the (dead) z image, + bias + x, ReLU,
+//      split-block stores.
+// HBM traffic per block: read x (+2 halo frames per 14, L2 hits for the
+// neighbour tiles), re-read x for the residual (L2-hot), write out.
+#include <type_traits>
+
+#include "cgemm3_dev.h"
+
+namespace tik {
+
+template <int CIN, int COUT, int FIN>
+struct StbGeo {
+    static constexpr int V = 17;
+    static constexpr int F = FIN - 2;   // output frames per tile
+    static constexpr int PX = FIN * V, PXB = V, PXR = PX;   // pixel block j = joint j of the FIN frames
+    static constexpr int ZR = PX, ZROWS = PX + 1;          // zero row of each z block image
+    static constexpr int TR = F * V, TRB = (TR + 15) / 16;
+    static constexpr int NKG = CIN / 32, NKB = COUT / 32, NKT = 3 * NKB;
+    static constexpr int ZB = ZROWS * 128, ZBYTES = NKB * ZB;
+    static constexpr int XS = PXR * 128, WS = COUT * 128;
+    static constexpr int GSLOT = XS + WS, RING = 2 * GSLOT;
+    static constexpr int TSLOTS = RING / WS < NKT ? RING / WS : NKT;
+    static constexpr int LDC = COUT + 4;
+    static constexpr int CT = TRB * 16 * LDC * 4;
+    static constexpr int SMEM = ZBYTES + RING;
+    static_assert(FIN == 16, "joint-major pixel blocks: 16 frames per block");
+    static_assert(COUT == 64, "G: one 16-channel block per wave for waves 0-3");
+    static_assert(CT <= ZBYTES, "C tile must fit over the z image");
+    static_assert(SMEM <= 163840, "LDS");
+    static_assert(TSLOTS >= 2, "T ring");
+};
+
+template <int CIN, int COUT, int FIN>
+__global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
+    using G = StbGeo<CIN, COUT, FIN>;
+    constexpr int V = 17;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM];   // the only LDS object
+    unsigned char* const zimg = smem;
+    unsigned char* const ring = smem + G::ZBYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4;
+    const int QO = a.nwin * a.T;   // frames (flat, input = output for stride 1)
+    const int M = QO * V;          // rows
+    int tile;
+    {   // XCD-aware tile order (cgemm3.hip): a contiguous run of tiles per XCD, so
+        // the halo frames a tile shares with its neighbours are L2 hits
+        const int nwg = gridDim.x, bid = blockIdx.x;
+        const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
+        tile = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+    }
+    unsigned long long tr[6];
+    if (a.trace) tr[0] = __builtin_amdgcn_s_memrealtime();
+    const int q0 = tile * G::F;   // first output frame
+    const int r0 = q0 * V;        // first output row
+    const int fi0 = q0 - 1;       // first input frame of the z image
+
+    // The mix matrix goes to registers before any DMA is issued (an LDS read
+    // after an LDS-DMA gets a compiler vmcnt(0): possible alias):
+    // amv[k] lane l = A[64 k + l], read back with v_readlane (wave-uniform).
+    constexpr int NAM = (V * V + 63) / 64;
+    float amv[NAM];
+#pragma unroll
+    for (int k = 0; k < NAM; ++k) amv[k] = 64 * k + lane < V * V ? a.amix[64 * k + lane] : 0.f;
+
+    // ---- DMA roles (lane l of an instruction writes unit l&7 of image row l>>3)
+    constexpr int NXI = G::PXR / 8, NXJ = (NXI + 7) / 8;   // x instructions per chunk / per wave (max)
+    constexpr int NWJ = COUT / 64;                          // Wg / Wt instructions per wave per chunk
+    unsigned xoff[NXJ];
+#pragma unroll
+    for (int j = 0; j < NXJ; ++j) {
+        const int idx = wave + 8 * j;
+        const int rr = idx * 8 + (lane >> 3);   // image row: joint rr / 16, frame rr % 16
+        const int ck = (lane & 7) ^ sbf(rr);
+        const long long gr = (long long)(fi0 + (rr & 15)) * V + (rr >> 4);
+        xoff[j] = (idx < NXI && fi0 + (rr & 15) >= 0 && gr < M) ? (unsigned)((gr * a.ldx + 8 * ck) * 2) : DMA_OOB;
+    }
+    const int nxj = (NXI - wave + 7) / 8;   // x instructions of this wave
+    unsigned wgoff[NWJ], wtoff[NWJ];
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j) {
+        const int rr = (wave * NWJ + j) * 8 + (lane >> 3);
+        const int ck = (lane & 7) ^ sbf(rr);
+        wgoff[j] = (unsigned)((rr * a.ldwg + 8 * ck) * 2);
+        wtoff[j] = (unsigned)((rr * a.ldwt + 8 * ck) * 2);
+    }
+    const i32x4 rX = buf_rsrc(a.x, (unsigned)((long long)M * a.ldx * 2));
+    const i32x4 rWg = buf_rsrc(a.wg, (unsigned)(COUT * a.ldwg * 2));
+    const i32x4 rWt = buf_rsrc(a.wt, (unsigned)(COUT * a.ldwt * 2));
+
+    auto issue_g = [&](int kb, int slot) {
+        unsigned char* xs = ring + slot * G::GSLOT;
+#pragma unroll
+        for (int j = 0; j < NXJ; ++j)
+            if (wave + 8 * j < NXI) dma16(rX, xs + (wave + 8 * j) * 1024, xoff[j], kb * 128);
+#pragma unroll
+        for (int j = 0; j < NWJ; ++j) dma16(rWg, xs + G::XS + (wave * NWJ + j) * 1024, wgoff[j], kb * 128);
+    };
+    auto issue_t = [&](int c, int slot) {
+        unsigned char* ws = ring + slot * G::WS;
+#pragma unroll
+        for (int j = 0; j < NWJ; ++j) dma16(rWt, ws + (wave * NWJ + j) * 1024, wtoff[j], c * 128);
+    };
+
+    // ================= 1. G: y^T = Wg'^T x^T; waves 0-3 own channel block `wave`, all 17 joints
+    const bool gw = wave < 4;
+    f32x4 accg[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) accg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue_g(0, 0);
+    if (G::NKG > 1) issue_g(1, 1);
+#pragma unroll
+    for (int kb = 0; kb < G::NKG; ++kb) {
+        if (kb + 1 < G::NKG) {   // chunk kb+1 may stay in flight
+            if (nxj == NXJ) wait_vm<NXJ + NWJ>();
+            else wait_vm<(NXJ > 0 ? NXJ - 1 : 0) + NWJ>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (gw) {
+            const unsigned char* X = ring + (kb & 1) * G::GSLOT;
+            const unsigned char* W = X + G::XS;
+            const int r = wave * 16 + (lane & 15);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(W + sbo(r, g));
+            const f16x8 al = *reinterpret_cast<const f16x8*>(W + sbo(r, 4 + g));
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const int rx = j * 16 + (lane & 15);
+                const f16x8 bh = *reinterpret_cast<const f16x8*>(X + sbo(rx, g));
+                const f16x8 bl = *reinterpret_cast<const f16x8*>(X + sbo(rx, 4 + g));
+                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, accg[j], 0, 0, 0);
+                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, accg[j], 0, 0, 0);
+                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, accg[j], 0, 0, 0);
+            }
+        }
+        if (kb + 2 < G::NKG) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            issue_g(kb + 2, kb & 1);
+        }
+    }
+    // bias2 of this lane's 4 channels for all joints: loaded before the Wt
+    // DMAs below so its wait does not queue behind them
+    const int mc = wave * 16 + 4 * g;   // mix channels mc .. mc+3 (waves 0-3)
+    f32x4 b2r[V];
+#pragma unroll
+    for (int w = 0; w < V; ++w)
+        b2r[w] = gw ? *reinterpret_cast<const f32x4*>(a.bias2 + w * COUT + mc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (a.trace) tr[1] = __builtin_amdgcn_s_memrealtime();
+    // the ring is free: the first Wt chunks load during the mix
+#pragma unroll
+    for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
+    if (a.trace) tr[2] = __builtin_amdgcn_s_memrealtime();
+
+    // ================= 2. mix in registers: z[w] = ReLU(bias2[w] + sum_v A[v][w] y[v])
+    if (gw) {
+        const int f = lane & 15, cc = mc & 31;
+        unsigned char* zb = zimg + (mc >> 5) * G::ZB + (cc & 4) * 2;
+        const int uh = cc >> 3;
+        auto mix_all = [&](auto sparse_tag) {
+            constexpr bool SP = decltype(sparse_tag)::value;
+#pragma unroll
+            for (int w = 0; w < V; ++w) {
+                f32x4 z = b2r[w];
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    if (!SP || ((coco_hop2_mask3(w) >> v) & 1u)) {
+                        const float av = __builtin_bit_cast(
+                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + w) / 64]), (v * V + w) % 64));
+                        z += av * accg[v];
+                    }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                f16x4 h, l;
+                split4(z, h, l);
+                const int row = f * V + w;
+                *reinterpret_cast<f16x4*>(zb + sbo(row, uh)) = h;
+                *reinterpret_cast<f16x4*>(zb + sbo(row, 4 + uh)) = l;
+            }
+        };
+        if (a.mix_sparse) mix_all(std::true_type{});
+        else mix_all(std::false_type{});
+    } else if (tid - 256 < G::NKB * 8) {   // zero rows (taps past a window edge)
+        const int i = tid - 256;
+        *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
+
+    // ================= 3. T: out = z (*) Wt over 3 taps, A from the resident z image
+    constexpr int NCGT = COUT / 64, WR = 8 / NCGT, NRB = (G::TRB + WR - 1) / WR;
+    const int cgt = wave % NCGT, wr = wave / NCGT;
+    int aoh[NRB][3], aol[NRB][3];
+#pragma unroll
+    for (int i = 0; i < NRB; ++i) {
+        const int rb = wr + WR * i;
+        const int m = rb * 16 + (lane & 15);
+        const int tl = m / V, v = m - tl * V;
+        const int q = q0 + tl;
+        const bool okm = rb < G::TRB && m < G::TR && q < QO;
+        const int to = okm ? q % a.T : 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int ti = to + k - 1;
+            const int zr = (okm && ti >= 0 && ti < a.T) ? (tl + k) * V + v : G::ZR;
+            aoh[i][k] = sbo(zr, g);
+            aol[i][k] = sbo(zr, 4 + g);
+        }
+    }
+    f32x4 acct[NRB][4];
+#pragma unroll
+    for (int i = 0; i < NRB; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acct[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int c = 0; c < G::NKT; ++c) {
+        const int tap = c / G::NKB, kb = c % G::NKB;
+        // chunk c retired; chunks c+1 .. c+TSLOTS-2 may stay in flight
+        const int younger = (G::TSLOTS - 2 < G::NKT - 1 - c) ? G::TSLOTS - 2 : G::NKT - 1 - c;
+        if (younger >= 4) wait_vm<4 * NWJ>();
+        else if (younger == 3) wait_vm<3 * NWJ>();
+        else if (younger == 2) wait_vm<2 * NWJ>();
+        else if (younger == 1) wait_vm<NWJ>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (c + G::TSLOTS - 1 < G::NKT) issue_t(c + G::TSLOTS - 1, (c + G::TSLOTS - 1) % G::TSLOTS);
+        const unsigned char* B = ring + (c % G::TSLOTS) * G::WS;
+        const unsigned char* A = zimg + kb * G::ZB;
+        f16x8 bh[4], bl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = cgt * 64 + j * 16 + (lane & 15);
+            bh[j] = *reinterpret_cast<const f16x8*>(B + sbo(r, g));
+            bl[j] = *reinterpret_cast<const f16x8*>(B + sbo(r, 4 + g));
+        }
+#pragma unroll
+        for (int i = 0; i < NRB; ++i) {
+            if (wr + WR * i < G::TRB) {
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(A + aoh[i][tap]);
+                const f16x8 al = *reinterpret_cast<const f16x8*>(A + aol[i][tap]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acct[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acct[i][j], 0, 0, 0);
+                    acct[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acct[i][j], 0, 0, 0);
+                    acct[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acct[i][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    if (a.trace) tr[4] = __builtin_amdgcn_s_memrealtime();
+    // ================= 4. epilogue: + bias + x, ReLU, split-block stores
+    constexpr int C4 = COUT / 4, RS = 512 / C4, KI = (G::TR + RS - 1) / RS;
+    const int c4 = tid % C4, lr0 = tid / C4, col = 4 * c4;
+    f32x4 rr[KI];   // raw residual halves (hi dwords 0-1, lo 2-3), loaded before the staging
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+        rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int lr = lr0 + k * RS;
+        if (a.resid && lr < G::TR && r0 + lr < M) {
+            const unsigned short* rp = a.x + (size_t)(r0 + lr) * a.ldx + sbc(col);
+            const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
+            const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
+            rr[k] = f32x4{h[0], h[1], l[0], l[1]};
+        }
+    }
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + col);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave is done reading z: the C tile goes over it
+    float* Cs = reinterpret_cast<float*>(zimg);
+#pragma unroll
+    for (int i = 0; i < NRB; ++i) {
+        if (wr + WR * i < G::TRB) {
+            const int crow = (wr + WR * i) * 16 + 4 * g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Cs[(crow + e) * G::LDC + cgt * 64 + j * 16 + (lane & 15)] = acct[i][j][e];
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // LDS only: the residual loads stay in flight
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+        const int lr = lr0 + k * RS, row = r0 + lr;
+        if (lr >= G::TR || row >= M) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * G::LDC + col) + bv;
+        const f16x4 h = __builtin_bit_cast(f16x4, f32x2{rr[k][0], rr[k][1]});
+        const f16x4 l = __builtin_bit_cast(f16x4, f32x2{rr[k][2], rr[k][3]});
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[e] += (float)h[e] + (float)l[e];
+            v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+        f16x4 oh, ol;
+        split4(v, oh, ol);
+        unsigned short* o = a.out + (size_t)row * a.ldo + sbc(col);
+        *reinterpret_cast<f16x4*>(o) = oh;
+        *reinterpret_cast<f16x4*>(o + 32) = ol;
+    }
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        tr[5] = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0)
+            for (int k = 0; k < 6; ++k) a.trace[6 * blockIdx.x + k] = tr[k];
+    }
+}
+
+bool stblock_ok(int cin, int cout) { return cin == 64 && cout == 64; }
+
+hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st) {
+    if (a.nwin <= 0 || a.T <= 0) return hipSuccess;
+    if (!stblock_ok(cin, cout) || !a.x || !a.wg || !a.wt || !a.bias || !a.bias2 || !a.amix || !a.out)
+        return hipErrorInvalidValue;
+    const long long M = (long long)a.nwin * a.T * 17;
+    if (a.ldx < 64 * (cin / 32) || a.ldo < 64 * (cout / 32) || a.ldx % 8 || a.ldo % 8 || a.ldwg < 64 * (cin / 32) ||
+        a.ldwt < 3 * 64 * (cout / 32) || a.ldwg % 8 || a.ldwt % 8 || M * a.ldx * 2 >= 0x80000000LL)
+        return hipErrorInvalidValue;
+    (void)hipGetLastError();
+    using G = StbGeo<64, 64, 16>;
+    const int QO = a.nwin * a.T;
+    hipLaunchKernelGGL((stblock_kernel<64, 64, 16>), dim3((QO + G::F - 1) / G::F), dim3(512), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace tik

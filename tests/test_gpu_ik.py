@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk"])
+@pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
+                                                 "f16x3-layered"])
 def model(request):
     """fp32 MFMA; f16x3 with the size-based choice of GEMM path (register-staged
     fp32 activations + split-K for small batches, split-plane activations with
@@ -26,8 +27,11 @@ def model(request):
     m = synthetic_model(win_size=64, device="cuda", precision=prec)
     if path:
         # "dmachunk": the DMA path with sub-batches of at most 3 windows (the
-        # 2 GiB-per-tensor split of large batches, exercised at test sizes)
-        env = {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"} if path == "dmachunk" else {"TIK_GEMM_PATH": path}
+        # 2 GiB-per-tensor split of large batches, exercised at test sizes);
+        # "layered": the DMA path with every block as separate G and T kernels
+        # (no whole-block stblock kernel)
+        env = {"dmachunk": {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"},
+               "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created

@@ -40,6 +40,14 @@ typedef struct {
 
 const char* tik_last_error(void);
 const char* tik_version(void);
+// Debug: with TIK_GUARD=1 in the environment every library buffer carries
+// 1 MiB guard zones; returns the number of written guard zones (description
+// in tik_last_error(), guards re-armed), or < 0 on error.
+int tik_debug_check_guards(void);
+// Debug: with TIK_CHECKSUM set, every launch of the IK forward is followed by
+// a synchronising checksum of its output; copies "label:hex;..." of the
+// launches since the last call into buf and clears the record.
+int tik_debug_checksums(char* buf, int len);
 
 /* ------------------------------------------------------------------------
  * IK model: PoseRegressor = StgGcn18 backbone + MLP head.

@@ -14,7 +14,7 @@ from typing import Dict, Iterable, Tuple
 import numpy as np
 import torch  # noqa: F401  (must precede loading libtik.so)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtik.so")
+LIB_PATH = os.environ.get("TIK_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtik.so")
 
 TIK_OK, TIK_E_INVALID, TIK_E_HIP, TIK_E_MISSING, TIK_E_NOMEM = 0, -1, -2, -3, -4
 
@@ -32,6 +32,8 @@ _F = ctypes.POINTER(ctypes.c_float)
 SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_last_error": (ctypes.c_char_p, ()),
     "tik_version": (ctypes.c_char_p, ()),
+    "tik_debug_check_guards": (_I, ()),
+    "tik_debug_checksums": (_I, (ctypes.c_char_p, _I)),
     "tik_model_create": (_I, (ctypes.POINTER(TikTensor), _I, ctypes.POINTER(_P))),
     "tik_model_destroy": (_I, (_P,)),
     "tik_model_out_frames": (_I, (_P, _I)),

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -27,6 +28,21 @@
 
 namespace tik_host {
 thread_local std::string g_err;
+
+bool guard_mode() {
+    static const bool on = getenv("TIK_GUARD") && getenv("TIK_GUARD")[0] == '1';
+    return on;
+}
+static std::mutex g_guard_mu;
+static std::map<void*, size_t> g_guard_bufs;   // base -> payload bytes
+void guard_register(void* base, size_t bytes) {
+    std::lock_guard<std::mutex> l(g_guard_mu);
+    g_guard_bufs[base] = bytes;
+}
+void guard_unregister(void* base) {
+    std::lock_guard<std::mutex> l(g_guard_mu);
+    g_guard_bufs.erase(base);
+}
 }
 using namespace tik_host;
 
@@ -71,6 +87,13 @@ tik::Seg3 mkseg3(const half_t* src, int ld, const SBW& w, int kt, int stride, in
 
 enum ResKind { RES_ZERO = 0, RES_IDEN = 1, RES_CONV = 2 };
 
+// debug hook (TIK_DRAIN bitmask): full vmcnt(0) drain before every K-step
+// barrier of the DMA kernels — 1 graph (G), 2 temporal (T), 4 head
+int drain_mask() {
+    static const int m = getenv("TIK_DRAIN") ? atoi(getenv("TIK_DRAIN")) : 0;
+    return m;
+}
+
 // Optional per-launch HIP-event profiler (bench.py's roofline numbers): one
 // event pair per kernel launch on the launch stream, algorithmic FLOPs and
 // bytes computed from the shapes.
@@ -112,13 +135,41 @@ struct Profiler {
 };
 thread_local Profiler* g_prof = nullptr;   // set for the duration of a profiled call
 
+// debug (TIK_CHECKSUM=1): after every annotated launch, synchronise and
+// record a checksum of its output buffer (tik_debug_checksums)
+static bool checksum_mode() {
+    static const bool on = getenv("TIK_CHECKSUM") != nullptr;
+    return on;
+}
+static std::string g_cks;
+static unsigned long long* g_cks_dev = nullptr;
+
 struct ProfScope {
     int i;
     hipStream_t st;
-    ProfScope(const char* label, double flops, double bytes, hipStream_t s) : st(s) {
+    const char* lab;
+    const void* op = nullptr;
+    size_t obytes = 0;
+    void out(const void* p, size_t bytes) { op = p; obytes = bytes; }
+    ProfScope(const char* label, double flops, double bytes, hipStream_t s) : st(s), lab(label) {
         i = g_prof ? g_prof->begin(label, flops, bytes, s) : -1;
     }
-    ~ProfScope() { if (g_prof) g_prof->end(i, st); }
+    ~ProfScope() {
+        if (g_prof) g_prof->end(i, st);
+        static const bool sync_each = getenv("TIK_SYNC_EACH") != nullptr;   // debug: serialise launches
+        if (sync_each) (void)hipStreamSynchronize(st);
+        if (checksum_mode() && op) {
+            if (!g_cks_dev) (void)hipMalloc(&g_cks_dev, 8);
+            unsigned long long h = 0;
+            (void)hipMemsetAsync(g_cks_dev, 0, 8, st);
+            (void)tik::launch_checksum(op, obytes, g_cks_dev, st);
+            (void)hipMemcpyAsync(&h, g_cks_dev, 8, hipMemcpyDeviceToHost, st);
+            (void)hipStreamSynchronize(st);
+            char b[160];
+            snprintf(b, sizeof(b), "%s:%llx;", lab, h);
+            g_cks += b;
+        }
+    }
 };
 
 // One StGcnBlock with BN folded into packed fp32 weights.
@@ -280,6 +331,7 @@ struct Layer {
         g.nseg = 1;
         g.bias = bias2.p; g.out_h = z; g.ldo = ldz; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
+        if (drain_mask() & 1) g.tune |= 2;
         const double px_in = (double)rin, px_out = (double)rout;
         if (!xraw && stride == 1 && res == RES_IDEN && V == 17 && tik::stblock_ok(cin, cout) && fuse) {
             // whole block in one kernel: z stays in LDS (stblock.hip)
@@ -293,6 +345,7 @@ struct Layer {
                         4.0 * (px_in * cin + px_out * cout + (double)cout * cin + (double)TK * cout * cout), st);
             static const bool trace = getenv("TIK_STB_TRACE") != nullptr;
             if (!trace) {
+                p.out(out, (size_t)rout * ldz * 2);
                 HIP_TRY(tik::launch_stblock(b, cin, cout, st));
                 return TIK_OK;
             }
@@ -321,6 +374,7 @@ struct Layer {
         if (xraw) {
             ProfScope p("G0_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout), st);
+            p.out(z, (size_t)rin * ldz * 2);
             HIP_TRY(tik::launch_gcn0(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
                                      cout, z, ldz, xb4, st));
         } else {
@@ -329,6 +383,7 @@ struct Layer {
             const std::string lab = std::string(wide ? "G3_272x128.L" : "G3_272x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+            p.out(z, (size_t)rin * ldz * 2);
             HIP_TRY(tik::launch_cgemm3(g, wide ? tik::C3_G272x128_W8 : tik::C3_G272x64, st));
         }
         tik::Cgemm3Args t{};
@@ -345,6 +400,7 @@ struct Layer {
         }
         t.bias = biasT.p; t.out_h = out; t.ldo = ldz; t.act = tik::ACT_RELU;
         t.zeros = zeros;
+        if (drain_mask() & 2) t.tune |= 2;
         const bool big = cout >= 128;
         double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
@@ -356,6 +412,7 @@ struct Layer {
         } else {
             const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
+            p.out(out, (size_t)rout * ldz * 2);
             HIP_TRY(tik::launch_tgemm(t, big ? tik::TG_128x128 : tik::TG_128x64, st));
         }
         return TIK_OK;
@@ -397,6 +454,46 @@ struct tik_block {
 extern "C" {
 
 const char* tik_last_error(void) { return g_err.c_str(); }
+
+int tik_debug_checksums(char* buf, int len) {
+    if (!checksum_mode()) return fail(TIK_E_INVALID, "TIK_CHECKSUM is not set");
+    const int n = (int)g_cks.size();
+    if (buf && len > 0) {
+        strncpy(buf, g_cks.c_str(), len - 1);
+        buf[len - 1] = 0;
+    }
+    g_cks.clear();
+    return n;
+}
+
+int tik_debug_check_guards(void) {
+    if (!guard_mode()) return fail(TIK_E_INVALID, "TIK_GUARD=1 is not set");
+    HIP_TRY(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> l(g_guard_mu);
+    std::vector<unsigned char> h(GUARD_BYTES);
+    int bad = 0;
+    std::string rep;
+    for (const auto& kv : g_guard_bufs) {
+        const char* base = static_cast<const char*>(kv.first);
+        for (int side = 0; side < 2; ++side) {
+            const char* gp = side == 0 ? base : base + GUARD_BYTES + kv.second;
+            HIP_TRY(hipMemcpy(h.data(), gp, GUARD_BYTES, hipMemcpyDeviceToHost));
+            size_t first = GUARD_BYTES, last = 0, cnt = 0;
+            for (size_t i = 0; i < GUARD_BYTES; ++i)
+                if (h[i] != 0xA5) { first = std::min(first, i); last = i; ++cnt; }
+            if (cnt) {
+                ++bad;
+                char b[256];
+                snprintf(b, sizeof(b), "[buf %p payload %zu B: %s guard, %zu bytes changed at +%zu..+%zu] ", (const void*)(base + GUARD_BYTES),
+                         kv.second, side == 0 ? "front" : "back", cnt, first, last);
+                rep += b;
+                HIP_TRY(hipMemset(const_cast<char*>(gp), 0xA5, GUARD_BYTES));
+            }
+        }
+    }
+    g_err = rep;
+    return bad;
+}
 const char* tik_version(void) { return "tik 0.2.0 (gfx950; fp32 MFMA and f16x3 split MFMA with LDS DMA)"; }
 
 int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out) {
@@ -624,18 +721,22 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
     h.seg[0] = mkseg3(f, m->V * ldf, m->sb0, 1, 1, 0, rows);
     h.nseg = 1; h.bias = m->b0.p; h.out_h = hs; h.ldo = ldh;
     h.act = tik::ACT_LEAKY; h.zeros = m->zeros.p;
+    if (drain_mask() & 4) h.tune |= 2;
     {
         ProfScope pr("H3_64x64.head0", 2.0 * rows * m->feat * m->hidden,
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
+        pr.out(hs, (size_t)rows * ldh * 2);
         HIP_TRY(tik::launch_cgemm3(h, tik::C3_H64x64, st));
     }
     tik::Cgemm3Args p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
     p.seg[0] = mkseg3(hs, ldh, m->sb3, 1, 1, 0, rows);
     p.nseg = 1; p.bias = m->b3.p; p.out_f = poses; p.ldf = m->pose_dim; p.act = tik::ACT_NONE; p.zeros = m->zeros.p;
+    if (drain_mask() & 4) p.tune |= 2;
     {
         ProfScope pr("H3_64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
+        pr.out(poses, (size_t)rows * m->pose_dim * 4);
         HIP_TRY(tik::launch_cgemm3(p, tik::C3_H64x64, st));
     }
     return TIK_OK;

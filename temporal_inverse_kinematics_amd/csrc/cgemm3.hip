@@ -43,13 +43,12 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
     // the DMA ring makes hipcc wait vmcnt(0) before the first ds_read of every
     // k-step, i.e. for the stage just issued, which serialises DMA and MFMA.
     constexpr int NB = (EPI == EPI_GRAPH) ? VT * BN : BN;
-    constexpr int NA = (EPI == EPI_GRAPH) ? VT * VT : 1;
-    constexpr int NBA = (NB + NA + 3) & ~3;
+    constexpr int NBA = (NB + 3) & ~3;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM + 4 * NBA];
     float* bias_s = reinterpret_cast<float*>(smem + SMEM);
-    float* amix_s = bias_s + NB;
 
     const int tid = threadIdx.x;
+    TIK_FENCE_BEGIN();
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
@@ -102,8 +101,13 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
         const int w = i / BN, col = n0 + i % BN;
         bias_s[i] = (a.bias && col < a.Nc) ? a.bias[w * a.Nc + col] : 0.f;
     }
-    if constexpr (EPI == EPI_GRAPH)
-        for (int i = threadIdx.x; i < NA; i += NT) amix_s[i] = a.amix[i];
+    // A_eff in registers (amv[k] lane l = A[64 k + l], read back with v_readlane):
+    // the mix reads no broadcast LDS constants (layer0.hip: such reads returned
+    // wrong elements when other kernels shared the CU)
+    constexpr int NAM = (EPI == EPI_GRAPH) ? (VT * VT + 63) / 64 : 1;
+    float amv[NAM];
+#pragma unroll
+    for (int k = 0; k < NAM; ++k) amv[k] = (EPI == EPI_GRAPH && 64 * k + lane < VT * VT) ? a.amix[64 * k + lane] : 0.f;
 
     int ktotal = a.seg[0].kt * a.seg[0].nblk;
     if (a.nseg > 1) ktotal += a.seg[1].kt * a.seg[1].nblk;
@@ -239,7 +243,9 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             const unsigned long long w0 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
             // this wave's DMA count per stage: NI, PN (one partial wave) or 0
             const int myn = min(NI, max(0, NIT - wave * NI));
-            if (NSTAGE >= 4 && ahead >= 2) {
+            if (a.tune & 2) {
+                wait_vm<0>();
+            } else if (NSTAGE >= 4 && ahead >= 2) {
                 if (myn == NI) wait_vm<(NSTAGE >= 4 ? 2 * NI : 0)>();
                 else if (myn == PN) wait_vm<(NSTAGE >= 4 ? 2 * PN : 0)>();
                 else wait_vm<0>();
@@ -315,7 +321,11 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
                     f32x4 z = *reinterpret_cast<const f32x4*>(bias_s + w * BN + 4 * c4);
 #pragma unroll
                     for (int v = 0; v < VT; ++v)
-                        if (!decltype(sparse)::value || ((coco_hop2_mask3(w) >> v) & 1u)) z += amix_s[v * VT + w] * y[v];
+                        if (!decltype(sparse)::value || ((coco_hop2_mask3(w) >> v) & 1u)) {
+                            const float av = __builtin_bit_cast(
+                                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * VT + w) / 64]), (v * VT + w) % 64));
+                            z += av * y[v];
+                        }
 #pragma unroll
                     for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
                     if (full) {
@@ -349,6 +359,7 @@ __global__ __launch_bounds__(64 * WM * WN) void cgemm3_kernel(Cgemm3Args a) {
             t[4] = tw_bar | ((unsigned long long)(tl1 - tl0) << 32);   // barrier cycles | loop cycles << 32
         }
     }
+    TIK_FENCE_END();
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int VT, int NSTAGE, int DBG = 0>

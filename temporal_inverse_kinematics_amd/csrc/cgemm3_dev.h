@@ -57,10 +57,23 @@ __device__ __forceinline__ i32x4 buf_rsrc(const void* p, unsigned bytes) {
 
 // 16 B per lane from rsrc + voff + soff into LDS at dst (wave-uniform base; lane l -> dst + 16 l)
 __device__ __forceinline__ void dma16(const i32x4 r, void* dst, unsigned voff, int soff) {
-    tik_llvm_raw_buffer_load_lds(r, (__attribute__((address_space(3))) unsigned*)dst, 16, (int)voff, soff, 0, 0);
+#ifndef TIK_DMA_AUX
+#define TIK_DMA_AUX 0
+#endif
+    tik_llvm_raw_buffer_load_lds(r, (__attribute__((address_space(3))) unsigned*)dst, 16, (int)voff, soff, 0, TIK_DMA_AUX);
 }
 
 constexpr unsigned DMA_OOB = 0x80000000u;
+
+// debug build hook (-DTIK_KFENCE): explicit agent-scope acquire at kernel
+// start / release at kernel end of the DMA-path kernels
+#ifdef TIK_KFENCE
+#define TIK_FENCE_BEGIN() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#define TIK_FENCE_END() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#else
+#define TIK_FENCE_BEGIN() ((void)0)
+#define TIK_FENCE_END() ((void)0)
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {

@@ -66,6 +66,33 @@ inline const HostTensor* find(const TensorMap& m, const std::string& k) {
     return it == m.end() ? nullptr : &it->second;
 }
 
+// Debug hook (TIK_GUARD=1): every device buffer gets 1 MiB guard zones on
+// both sides filled with 0xA5; tik_debug_check_guards() reports the first
+// buffer whose guards were written (an out-of-bounds store).
+constexpr size_t GUARD_BYTES = 1 << 20;
+bool guard_mode();
+void guard_register(void* base, size_t bytes);
+void guard_unregister(void* base);
+
+inline hipError_t dev_alloc(void** p, size_t bytes) {
+    if (!guard_mode()) return hipMalloc(p, bytes);
+    char* base = nullptr;
+    const size_t tot = bytes + 2 * GUARD_BYTES;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&base), tot);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(base, 0xA5, tot)) != hipSuccess) return e;
+    guard_register(base, bytes);
+    *p = base + GUARD_BYTES;
+    return hipSuccess;
+}
+inline void dev_free(void* p) {
+    if (!p) return;
+    if (!guard_mode()) { (void)hipFree(p); return; }
+    char* base = static_cast<char*>(p) - GUARD_BYTES;
+    guard_unregister(base);
+    (void)hipFree(base);
+}
+
 template <class T>
 struct DevArray {   // owning device buffer; move-only (a copy would double-free)
     T* p = nullptr;
@@ -76,25 +103,25 @@ struct DevArray {   // owning device buffer; move-only (a copy would double-free
     DevArray(DevArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
     DevArray& operator=(DevArray&& o) noexcept {
         if (this != &o) {
-            if (p) (void)hipFree(p);
+            dev_free(p);
             p = o.p; n = o.n; o.p = nullptr; o.n = 0;
         }
         return *this;
     }
-    ~DevArray() { if (p) (void)hipFree(p); }
+    ~DevArray() { dev_free(p); }
     int upload(const std::vector<T>& h) {
-        if (p) { (void)hipFree(p); p = nullptr; }
+        dev_free(p); p = nullptr;
         n = h.size();
         if (n == 0) return TIK_OK;
-        if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", h.size()); }
+        if (dev_alloc(reinterpret_cast<void**>(&p), n * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", h.size()); }
         if (hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
             return fail(TIK_E_HIP, "hipMemcpy H2D failed");
         return TIK_OK;
     }
     int reserve(size_t want) {
         if (want <= n) return TIK_OK;
-        if (p) { (void)hipFree(p); p = nullptr; }
-        if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", want); }
+        dev_free(p); p = nullptr;
+        if (dev_alloc(reinterpret_cast<void**>(&p), want * sizeof(T)) != hipSuccess) { n = 0; return fail(TIK_E_NOMEM, "hipMalloc(%zu elements) failed", want); }
         n = want;
         return TIK_OK;
     }

@@ -23,8 +23,8 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
     const int G = Cout / 4;            // channel groups per frame
     const int FPB = 256 / G;           // frames per workgroup
     __shared__ float xs[256 / 4 * VT * 4];   // up to 64 frames x 17 joints x 4 channels
-    __shared__ float am[VT * VT];
     const int tid = threadIdx.x;
+    TIK_FENCE_BEGIN();
     const int nframes = rows / VT;
     const int f0 = blockIdx.x * FPB;
     for (int i = tid; i < FPB * VT * 4; i += 256) {
@@ -35,7 +35,12 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
         xs[i] = val;
         if (fr < nframes) xb4[((size_t)fr * VT + v) * 4 + c] = val;
     }
-    for (int i = tid; i < VT * VT; i += 256) am[i] = amix[i];
+    // the mix matrix in registers (amv[k] lane l = A[64 k + l], read back with
+    // v_readlane): wave-uniform operands, no broadcast LDS reads in the mix
+    constexpr int NAM = (VT * VT + 63) / 64;
+    float amv[NAM];
+#pragma unroll
+    for (int k = 0; k < NAM; ++k) amv[k] = 64 * k + (tid & 63) < VT * VT ? amix[64 * k + (tid & 63)] : 0.f;
     __syncthreads();
 
     const int f = tid / G, g = tid - f * G;
@@ -64,7 +69,11 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
         f32x4 z = b[wj];
 #pragma unroll
         for (int v = 0; v < VT; ++v)
-            if (!SPARSE || ((coco_hop2_mask3(wj) >> v) & 1u)) z += am[v * VT + wj] * y[v];
+            if (!SPARSE || ((coco_hop2_mask3(wj) >> v) & 1u)) {
+                const float av = __builtin_bit_cast(
+                    float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * VT + wj) / 64]), (v * VT + wj) % 64));
+                z += av * y[v];
+            }
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
         f16x4 h, l;
@@ -73,6 +82,7 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
         *reinterpret_cast<f16x4*>(o) = h;
         *reinterpret_cast<f16x4*>(o + 32) = l;
     }
+    TIK_FENCE_END();
 }
 
 hipError_t launch_gcn0(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,

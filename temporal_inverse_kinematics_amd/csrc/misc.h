@@ -18,4 +18,7 @@ hipError_t launch_stream_push(float* ring, int W, int nv, int* count, const floa
 hipError_t launch_stream_window(const float* ring, int W, int V, const int* count, int h, int ra, int rb,
                                 int relative, float* out, hipStream_t st);
 
+// debug: order-independent checksum (sum of 32-bit words, index-weighted) of a buffer into *out
+hipError_t launch_checksum(const void* p, size_t bytes, unsigned long long* out, hipStream_t st);
+
 }  // namespace tik

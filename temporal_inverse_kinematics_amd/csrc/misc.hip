@@ -218,4 +218,17 @@ hipError_t launch_stream_window(const float* ring, int W, int V, const int* coun
     return hipGetLastError();
 }
 
+__global__ void checksum_kernel(const unsigned* __restrict__ p, size_t n, unsigned long long* out) {
+    unsigned long long c = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c += (unsigned long long)p[i] * (2 * (i & 0xffff) + 1);
+    if (c) atomicAdd(out, c);
+}
+
+hipError_t launch_checksum(const void* p, size_t bytes, unsigned long long* out, hipStream_t st) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(checksum_kernel, dim3(1024), dim3(256), 0, st, static_cast<const unsigned*>(p), bytes / 4, out);
+    return hipGetLastError();
+}
+
 }  // namespace tik

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     unsigned char* const ring = smem + G::ZBYTES;
 
     const int tid = threadIdx.x, lane = tid & 63;
+    TIK_FENCE_BEGIN();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4;
     const int QO = a.nwin * a.T;   // frames (flat, input = output for stride 1)
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
         if (tid == 0)
             for (int k = 0; k < 6; ++k) a.trace[6 * blockIdx.x + k] = tr[k];
     }
+    TIK_FENCE_END();
 }
 
 bool stblock_ok(int cin, int cout) { return cin == 64 && cout == 64; }

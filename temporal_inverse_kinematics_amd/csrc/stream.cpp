@@ -58,7 +58,7 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
     s->h = win_size / 2;
     s->W = 2 * s->h + 1;
     s->tout = tik_model_out_frames(model, s->W);
-    int rc;
+    int rc = 0;
     if (s->tout <= 0 || (rc = tik_model_reserve(model, 1, s->W)) || (rc = s->ring.reserve((size_t)s->W * s->V * 3)) ||
         (rc = s->window.reserve((size_t)s->W * s->V * 3)) || (rc = s->poses.reserve((size_t)s->tout * s->pose_dim)) ||
         (rc = s->frame_in.reserve((size_t)s->V * 3)) || (rc = s->count.reserve(1))) {

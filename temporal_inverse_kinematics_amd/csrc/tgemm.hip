@@ -33,6 +33,7 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];   // the only LDS object
 
     const int tid = threadIdx.x, lane = tid & 63;
+    TIK_FENCE_BEGIN();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     int r0, n0;
@@ -117,16 +118,20 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
     auto issue_a = [&](int slot) {   // A stage of cursor ca, then advance it
         a_prepare();
         unsigned char* dst = smem + slot * ASLOT + wave * NIA * 1024;
+        // soffset through readfirstlane: the cursor is uniform but not provably so,
+        // and a VGPR soffset makes hipcc wrap every DMA in a waterfall loop
+        const int soA = __builtin_amdgcn_readfirstlane(ca.blk * 128);
 #pragma unroll
-        for (int j = 0; j < NIA; ++j) dma16(rA, dst + j * 1024, a_off[j], ca.blk * 128);
+        for (int j = 0; j < NIA; ++j) dma16(rA, dst + j * 1024, a_off[j], soA);
         step(ca);
     };
     auto issue_b = [&](int slot) {
         b_prepare();
         const int nb = cb.seg == 0 ? a.seg[0].nblk : a.seg[1].nblk;
         unsigned char* dst = smem + NSA * ASLOT + slot * BSLOT + wave * NIB * 1024;
+        const int soB = __builtin_amdgcn_readfirstlane((cb.tap * nb + cb.blk) * 128);
 #pragma unroll
-        for (int j = 0; j < NIB; ++j) dma16(rB, dst + j * 1024, b_off[j], (cb.tap * nb + cb.blk) * 128);
+        for (int j = 0; j < NIB; ++j) dma16(rB, dst + j * 1024, b_off[j], soB);
         step(cb);
     };
 
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
             // in flight (issue order): A(ch) .. | B(ch) | A(ch+1) .. A(ch+NSA-2):
             // retire everything up to B(ch), leave the younger A stages
             const int younger = min(NSA - 2, ktotal - 1 - ch);
-            if (NSA >= 3 && younger >= 1) wait_vm<(NSA >= 3 ? NIA : 0)>();
+            if (NSA >= 3 && younger >= 1 && !(a.tune & 2)) wait_vm<(NSA >= 3 ? NIA : 0)>();
             else wait_vm<0>();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const unsigned long long w1 = a.trace ? __builtin_amdgcn_s_memtime() : 0;
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
             t[4] = tw_bar | ((unsigned long long)(tl1 - tl0) << 32);
         }
     }
+    TIK_FENCE_END();
 }
 
 template <int BM, int BN, int WM, int WN, int NSA>

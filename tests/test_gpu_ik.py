@@ -177,3 +177,33 @@ def test_model_dma_subbatches_past_2gib(model):
         solo = torch.cat([model(x[i:i + 1])["poses"] for i in pick])
     assert torch.isfinite(y).all()
     assert (y[pick] - solo).abs().max().item() < 2e-5
+
+
+def test_concurrent_streams_bitwise():
+    """Four model handles on four HIP streams running concurrently give the
+    same poses, bit for bit, as the serial runs (regression: layer 0's graph
+    mix once read its constants as broadcast LDS loads and returned wrong
+    elements when other IK kernels shared the CUs)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    S = 4
+    x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=0)).cuda()
+    parts = list(x.chunk(S))
+    with torch.no_grad():
+        models = [synthetic_model(win_size=64, device="cuda").regressor for _ in range(S)]
+        ref = [models[i](parts[i])["poses"].clone() for i in range(S)]
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream() for _ in range(S)]
+        for _ in range(12):
+            ev = torch.cuda.Event()
+            ev.record()
+            outs = []
+            for i in range(S):
+                with torch.cuda.stream(streams[i]):
+                    streams[i].wait_event(ev)
+                    outs.append(models[i](parts[i])["poses"])
+            for s in streams:
+                torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            for i in range(S):
+                assert torch.equal(outs[i], ref[i])

@@ -33,8 +33,9 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 KERNEL_SYMBOLS = {
     "G3_272x128": "tik::cgemm3_kernel<272, 128, 1, 8, 1, 17, 3, 0>",
     "G3_272x64": "tik::cgemm3_kernel<272, 64, 1, 4, 1, 17, 1, 0>",
-    "T3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3>",
-    "T3_128x64": "tik::tgemm_kernel<128, 64, 4, 2, 3>",
+    "T3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 0>",
+    "T3_128x64": "tik::tgemm_kernel<128, 64, 4, 2, 3, 0>",
+    "TG3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 7>",
     "TH_128x128": "tik::tconv_halo_kernel<128, 2, 4>",
     "TH_128x64": "tik::tconv_halo_kernel<64, 4, 2>",
     "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",

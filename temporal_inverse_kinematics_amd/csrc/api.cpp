@@ -319,9 +319,17 @@ struct Layer {
                256 % (cout / 4) == 0;
     }
 
+    // this block's temporal conv can carry block n's gcn in its epilogue
+    // (TG_128x128_G7: 128 output channels in one tile; n: 128 -> 128, not a raw/whole-block layer)
+    bool can_fuse_next(const Layer& n) const {
+        return V == 17 && n.V == 17 && cout == 128 && n.cin == 128 && n.cout == 128 && n.index != 0 && sbt.nblk == 4 &&
+               n.sbg.nblk == 4;
+    }
+
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
                  bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
-                 const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true) const {
+                 const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true, const Layer* nxt = nullptr,
+                 half_t* znext = nullptr, bool zready = false) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -371,7 +379,9 @@ struct Layer {
                     ph[4] / nwg / 100, (hi - lo) / 100.0);
             return TIK_OK;
         }
-        if (xraw) {
+        if (zready) {
+            // z was written by the previous block's fused temporal-conv epilogue
+        } else if (xraw) {
             ProfScope p("G0_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout), st);
             p.out(z, (size_t)rin * ldz * 2);
@@ -405,7 +415,39 @@ struct Layer {
         double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
-        if (use_halo && tik::tconv_halo_ok(t)) {   // stride 1: taps share one LDS frame halo (tconv.hip)
+        if (nxt) {
+            // + the next block's gcn in the epilogue (TG_128x128_G7): its z is written here
+            t.g_w = nxt->sbg.w.p; t.g_ldw = nxt->sbg.ldw; t.g_nc = nxt->cout; t.g_bias2 = nxt->bias2.p;
+            t.g_amix = nxt->amix.p; t.g_mix_sparse = nxt->mix_sparse ? 1 : 0; t.g_out = znext;
+            t.g_ldo = 64 * nxt->sbt.nblk;
+            fl += 2.0 * px_out * cout * nxt->cout + 2.0 * V * px_out * nxt->cout;
+            by += 4.0 * (px_out * nxt->cout + (double)nxt->cout * cout + (double)V * (V + nxt->cout));
+            const std::string lab = std::string("TG3_128x128.L") + std::to_string(index);
+            static const bool trace = getenv("TIK_TG_TRACE") != nullptr;   // debug: per-phase workgroup timing
+            const int nwg = (int)((rout + 118) / 119);
+            unsigned long long* d = nullptr;
+            if (trace) {
+                HIP_TRY(hipMalloc(&d, (size_t)nwg * 8 * 8));
+                t.trace = d;
+            }
+            {
+                ProfScope p(lab.c_str(), fl, by, st);
+                p.out(out, (size_t)rout * ldz * 2);
+                HIP_TRY(tik::launch_tgemm(t, tik::TG_128x128_G7, st));
+            }
+            if (trace) {
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<unsigned long long> h((size_t)nwg * 8);
+                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipFree(d));
+                double ph[7] = {0, 0, 0, 0, 0, 0, 0};
+                for (int w = 0; w < nwg; ++w)
+                    for (int k = 0; k < 7; ++k) ph[k] += (double)(h[8 * w + k + 1] - h[8 * w + k]);
+                fprintf(stderr, "TG L%d (%d wg): per-wg us loop %.2f stageC %.2f image+Wg %.2f gcn %.2f out+stageZ %.2f mix %.2f tail %.2f\n",
+                        index, nwg, ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100,
+                        ph[4] / nwg / 100, ph[5] / nwg / 100, ph[6] / nwg / 100);
+            }
+        } else if (use_halo && tik::tconv_halo_ok(t)) {   // stride 1: taps share one LDS frame halo (tconv.hip)
             const std::string lab = std::string(big ? "TH_128x128.L" : "TH_128x64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), fl, by, st);
             HIP_TRY(tik::launch_tconv_halo(t, big ? 128 : 64, st));
@@ -430,12 +472,13 @@ struct tik_model {
     SplitW sw0, sw3;
     SBW sb0, sb3;
     int prec = 1;
-    DevBuf xb, z, a0, a1, hid;     // workspace
+    DevBuf xb, z, z2, a0, a1, hid; // workspace (z, z2: ping-pong for the fused T+G launches)
     DevBuf part;                   // split-K partial sums (small-batch launches)
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
     int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
     bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
+    bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
     Profiler prof;
     bool profiling = false;
 };
@@ -567,6 +610,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     }
     if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
     if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
+    if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
         else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
@@ -605,7 +649,7 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
     int rc;
-    if ((rc = m->xb.reserve((size_t)N * T * V * 32)) || (rc = m->z.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
+    if ((rc = m->xb.reserve((size_t)N * T * V * 32)) || (rc = m->z.reserve(zmax)) || (rc = m->z2.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
         (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
         return rc;
     return TIK_OK;
@@ -670,12 +714,20 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
     int ld = 64, t = T, rc;
     half_t* bufs[2] = {reinterpret_cast<half_t*>(m->a0.p), reinterpret_cast<half_t*>(m->a1.p)};
     int which = 0;
-    for (const Layer& L : m->layers) {
+    half_t* zb[2] = {reinterpret_cast<half_t*>(m->z.p), reinterpret_cast<half_t*>(m->z2.p)};
+    int zi = 0;
+    bool zready = false;
+    for (size_t li = 0; li < m->layers.size(); ++li) {
+        const Layer& L = m->layers[li];
         half_t* o = bufs[which];
-        const bool raw = &L == &m->layers.front() && L.raw_ok() && L.cin == m->C0;
-        if ((rc = L.forward3(cur, ld, N, t, reinterpret_cast<half_t*>(m->z.p), o, m->zeros.p, st, false,
-                             raw ? x : nullptr, m->bn_sc.p, m->bn_sh.p, m->xb.p, m->stblock)))
+        const bool raw = li == 0 && L.raw_ok() && L.cin == m->C0;
+        const Layer* nxt = (m->fuse_tg && li + 1 < m->layers.size() && L.can_fuse_next(m->layers[li + 1]))
+                               ? &m->layers[li + 1] : nullptr;
+        if ((rc = L.forward3(cur, ld, N, t, zb[zi], o, m->zeros.p, st, false, raw ? x : nullptr, m->bn_sc.p,
+                             m->bn_sh.p, m->xb.p, m->stblock, nxt, zb[zi ^ 1], zready)))
             return rc;
+        zready = nxt != nullptr;
+        if (nxt) zi ^= 1;
         t = Layer::tout(t, L.stride);
         cur = o; ld = 64 * L.sbt.nblk; which ^= 1;
     }

@@ -45,6 +45,15 @@ struct Cgemm3Args {
     int act;
     int mix_sparse;
     const unsigned short* zeros;  // >= 128 B of zeros: source of padded rows
+    // TG_128x128_G7 (tgemm.hip): the NEXT block's gcn (1x1 conv + graph mix +
+    // folded BN + ReLU) on this launch's output tile; null g_w = off
+    const unsigned short* g_w;    // SB weights of the next gcn [g_nc][g_ldw], K = Nc
+    int g_ldw, g_nc;
+    const float* g_bias2;         // [V][g_nc]
+    const float* g_amix;          // [V][V]
+    int g_mix_sparse;
+    unsigned short* g_out;        // SB z of the next block [M][g_ldo]
+    int g_ldo;
     int tune;                     // tuning experiments (0 = production): 1 plain tile order
                                   // instead of the XCD-aware one
     unsigned long long* trace;    // tuning only: per-workgroup {start, loop end, end, wait clk, barrier|loop clk}
@@ -71,6 +80,7 @@ enum TgemmCfg {
     TG_128x128_A4 = 2,   // A ring 4 (one workgroup per CU)
     TG_128x64_A4 = 3,
     TG_64x64 = 4,        // head Linear layers, 4 waves
+    TG_128x128_G7 = 5,   // 7-frame tiles (119 of 128 rows) + the next block's gcn in the epilogue
 };
 hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st);
 

@@ -14,7 +14,7 @@ TOL = 1e-4
 
 
 @pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
-                                                 "f16x3-layered"])
+                                                 "f16x3-layered", "f16x3-nofuse"])
 def model(request):
     """fp32 MFMA; f16x3 with the size-based choice of GEMM path (register-staged
     fp32 activations + split-K for small batches, split-plane activations with
@@ -29,9 +29,11 @@ def model(request):
         # "dmachunk": the DMA path with sub-batches of at most 3 windows (the
         # 2 GiB-per-tensor split of large batches, exercised at test sizes);
         # "layered": the DMA path with every block as separate G and T kernels
-        # (no whole-block stblock kernel)
+        # (no whole-block stblock kernel); "nofuse": the DMA path without the next
+        # block's gcn fused into the temporal-conv epilogue (separate G launches)
         env = {"dmachunk": {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"},
-               "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"}}.get(path, {"TIK_GEMM_PATH": path})
+               "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"},
+               "nofuse": {"TIK_GEMM_PATH": "dma", "TIK_FUSE_TG": "0"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created
@@ -207,3 +209,24 @@ def test_concurrent_streams_bitwise():
             torch.cuda.synchronize()
             for i in range(S):
                 assert torch.equal(outs[i], ref[i])
+
+
+def test_fused_gcn_epilogue_bitwise():
+    """The next block's gcn fused into the temporal-conv epilogue
+    (TG_128x128_G7) uses the separate G kernel's products and K order: the
+    poses are bit-identical with and without the fusion (1024 x 64 and
+    batches whose last tile is partial)."""
+    import os
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    fused = synthetic_model(win_size=64, device="cuda").regressor
+    os.environ["TIK_FUSE_TG"] = "0"
+    try:
+        plain = synthetic_model(win_size=64, device="cuda").regressor
+        plain.tik_handle()
+    finally:
+        del os.environ["TIK_FUSE_TG"]
+    for n, T in [(1024, 64), (333, 64), (70, 65)]:
+        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n)).cuda()
+        with torch.no_grad():
+            assert torch.equal(fused(x)["poses"], plain(x)["poses"]), (n, T)

@@ -40,7 +40,8 @@ KERNEL_SYMBOLS = {
     "TH_128x64": "tik::tconv_halo_kernel<64, 4, 2>",
     "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",
     "G0_raw": "tik::gcn0_kernel<1>",
-    "B3_64": "tik::stblock_kernel<64, 64, 16>",
+    "B3_64": "tik::stblock_kernel<64, 64, 16, false>",
+    "B0_64": "tik::stblock_kernel<64, 64, 16, true>",
 }
 
 

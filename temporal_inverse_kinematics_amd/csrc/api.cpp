@@ -379,6 +379,20 @@ struct Layer {
                     ph[4] / nwg / 100, (hi - lo) / 100.0);
             return TIK_OK;
         }
+        if (xraw && fuse && stride == 1 && res == RES_CONV && V == 17 && cout == 64 && wr0.p) {
+            // the whole first block from the raw keypoints in one kernel (stblock.hip, RAW)
+            tik::StbArgs b{};
+            b.nwin = N; b.T = tin;
+            b.bias2 = bias2.p; b.amix = amix.p; b.mix_sparse = mix_sparse ? 1 : 0;
+            b.wt = sbt.w.p; b.ldwt = sbt.ldw; b.bias = biasT.p; b.out = out; b.ldo = ldz;
+            b.xraw = xraw; b.c0 = cin; b.bn_sc = bn_sc; b.bn_sh = bn_sh; b.wg0 = wg.p; b.ldwg0 = cinp; b.rw = wr0.p;
+            ProfScope p("B0_64.L0",
+                        2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * (TK * cout + cin) * cout,
+                        4.0 * (px_in * cin + px_out * cout + (double)TK * cout * cout), st);
+            p.out(out, (size_t)rout * ldz * 2);
+            HIP_TRY(tik::launch_stblock0(b, cout, st));
+            return TIK_OK;
+        }
         if (zready) {
             // z was written by the previous block's fused temporal-conv epilogue
         } else if (xraw) {

@@ -117,9 +117,19 @@ struct StbArgs {
     unsigned short* out;
     int ldo;
     unsigned long long* trace;  // optional: 6 s_memrealtime stamps per workgroup (phase boundaries)
+    // raw-input first block (launch_stblock0): z from the keypoints in VALU, residual conv from them too
+    const float* xraw;          // [rows][c0] keypoints
+    int c0;                     // <= 4 input channels
+    const float* bn_sc;         // data_bn per (joint, channel) [17][c0]
+    const float* bn_sh;
+    const float* wg0;           // fp32 gcn weights (tcn.0 BN folded) [Cout][ldwg0]
+    int ldwg0;
+    const float* rw;            // fp32 residual conv (BN folded) [Cout][c0]
 };
 bool stblock_ok(int cin, int cout);
 hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st);
+// the whole FIRST block from the raw keypoints (Cout = 64, stride 1, residual conv)
+hipError_t launch_stblock0(const StbArgs& a, int cout, hipStream_t st);
 
 hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st);
 // data_bn on load, straight to one SB block per pixel (C <= 32 channels, rest zero) (st_gcn_aaai18.py:119-125)

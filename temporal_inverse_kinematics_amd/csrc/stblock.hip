@@ -51,11 +51,18 @@ struct StbGeo {
     static_assert(TSLOTS >= 2, "T ring");
 };
 
-template <int CIN, int COUT, int FIN>
+// RAW: the first block straight from the raw keypoints (layer0.hip's gcn0
+// math in VALU writes the z image; data_bn'd keypoints of the tile's 16
+// frames stay in LDS for the 3 -> Cout residual conv of the epilogue): the
+// block reads 12 B and writes 256 B per pixel, against the 256 + 768 B of
+// the gcn0 + temporal-conv pair.
+template <int CIN, int COUT, int FIN, bool RAW = false>
 __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     using G = StbGeo<CIN, COUT, FIN>;
     constexpr int V = 17;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM];   // the only LDS object
+    constexpr int XSB = RAW ? FIN * V * 4 * 4 : 0;   // data_bn'd keypoints, 4 floats per pixel
+    static_assert(G::SMEM + XSB <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM + XSB];   // the only LDS object
     unsigned char* const zimg = smem;
     unsigned char* const ring = smem + G::ZBYTES;
 
@@ -125,95 +132,163 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
         for (int j = 0; j < NWJ; ++j) dma16(rWt, ws + (wave * NWJ + j) * 1024, wtoff[j], c * 128);
     };
 
-    // ================= 1. G: y^T = Wg'^T x^T; waves 0-3 own channel block `wave`, all 17 joints
-    const bool gw = wave < 4;
-    f32x4 accg[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) accg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    issue_g(0, 0);
-    if (G::NKG > 1) issue_g(1, 1);
-#pragma unroll
-    for (int kb = 0; kb < G::NKG; ++kb) {
-        if (kb + 1 < G::NKG) {   // chunk kb+1 may stay in flight
-            if (nxj == NXJ) wait_vm<NXJ + NWJ>();
-            else wait_vm<(NXJ > 0 ? NXJ - 1 : 0) + NWJ>();
-        } else {
-            wait_vm<0>();
+    float* const xsf = reinterpret_cast<float*>(smem + G::SMEM);
+    if constexpr (RAW) {
+        // ================= 1'. G from the raw keypoints: data_bn(x) of the 16 frames -> LDS
+        for (int i = tid; i < FIN * V * 4; i += 512) {
+            const int c = i & 3, p = i >> 2;
+            const int v = p % V, fr = fi0 + p / V;
+            float val = 0.f;
+            if (c < a.c0 && fr >= 0 && fr < QO) val = fmaf(a.xraw[((size_t)fr * V + v) * a.c0 + c], a.bn_sc[v * a.c0 + c], a.bn_sh[v * a.c0 + c]);
+            xsf[i] = val;
         }
+        __syncthreads();
+        if (tid < 256) {
+            // (frame f, channels co..co+3) x all 17 joints, the gcn0 arithmetic
+            const int f = tid & 15, co = 4 * (tid >> 4);
+            float w[4][4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? a.wg0[(co + e) * a.ldwg0 + c] : 0.f;
+            f32x4 y[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const float* xp = xsf + (f * V + v) * 4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[v][e] = xp[0] * w[e][0] + xp[1] * w[e][1] + xp[2] * w[e][2] + xp[3] * w[e][3];
+            }
+            f32x4 b[V];
+#pragma unroll
+            for (int wj = 0; wj < V; ++wj) b[wj] = *reinterpret_cast<const f32x4*>(a.bias2 + wj * COUT + co);
+            const int cc = co & 31;
+            unsigned char* zb = zimg + (co >> 5) * G::ZB + (cc & 4) * 2;
+            const int uh = cc >> 3;
+            auto mix_all = [&](auto sparse_tag) {
+                constexpr bool SP = decltype(sparse_tag)::value;
+#pragma unroll
+                for (int wj = 0; wj < V; ++wj) {
+                    f32x4 z = b[wj];
+#pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
+                            const float av = __builtin_bit_cast(
+                                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + wj) / 64]), (v * V + wj) % 64));
+                            z += av * y[v];
+                        }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                    f16x4 h, l;
+                    split4(z, h, l);
+                    const int row = f * V + wj;
+                    *reinterpret_cast<f16x4*>(zb + sbo(row, uh)) = h;
+                    *reinterpret_cast<f16x4*>(zb + sbo(row, 4 + uh)) = l;
+                }
+            };
+            if (a.mix_sparse) mix_all(std::true_type{});
+            else mix_all(std::false_type{});
+        } else if (tid - 256 < G::NKB * 8) {   // zero rows (taps past a window edge)
+            const int i = tid - 256;
+            *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (a.trace) tr[1] = tr[2] = __builtin_amdgcn_s_memrealtime();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (gw) {
-            const unsigned char* X = ring + (kb & 1) * G::GSLOT;
-            const unsigned char* W = X + G::XS;
-            const int r = wave * 16 + (lane & 15);
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(W + sbo(r, g));
-            const f16x8 al = *reinterpret_cast<const f16x8*>(W + sbo(r, 4 + g));
+        // the ring is free: the first Wt chunks (the T loop's first wait covers them)
 #pragma unroll
-            for (int j = 0; j < V; ++j) {
-                const int rx = j * 16 + (lane & 15);
-                const f16x8 bh = *reinterpret_cast<const f16x8*>(X + sbo(rx, g));
-                const f16x8 bl = *reinterpret_cast<const f16x8*>(X + sbo(rx, 4 + g));
-                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, accg[j], 0, 0, 0);
-                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, accg[j], 0, 0, 0);
-                accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, accg[j], 0, 0, 0);
-            }
-        }
-        if (kb + 2 < G::NKG) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            issue_g(kb + 2, kb & 1);
-        }
-    }
-    // bias2 of this lane's 4 channels for all joints: loaded before the Wt
-    // DMAs below so its wait does not queue behind them
-    const int mc = wave * 16 + 4 * g;   // mix channels mc .. mc+3 (waves 0-3)
-    f32x4 b2r[V];
-#pragma unroll
-    for (int w = 0; w < V; ++w)
-        b2r[w] = gw ? *reinterpret_cast<const f32x4*>(a.bias2 + w * COUT + mc) : f32x4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (a.trace) tr[1] = __builtin_amdgcn_s_memrealtime();
-    // the ring is free: the first Wt chunks load during the mix
-#pragma unroll
-    for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
-    if (a.trace) tr[2] = __builtin_amdgcn_s_memrealtime();
+        for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
+        if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
+    } else {
+        // ================= 1. G: y^T = Wg'^T x^T; waves 0-3 own channel block `wave`, all 17 joints
+        const bool gw = wave < 4;
+        f32x4 accg[V];
+    #pragma unroll
+        for (int j = 0; j < V; ++j) accg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ================= 2. mix in registers: z[w] = ReLU(bias2[w] + sum_v A[v][w] y[v])
-    if (gw) {
-        const int f = lane & 15, cc = mc & 31;
-        unsigned char* zb = zimg + (mc >> 5) * G::ZB + (cc & 4) * 2;
-        const int uh = cc >> 3;
-        auto mix_all = [&](auto sparse_tag) {
-            constexpr bool SP = decltype(sparse_tag)::value;
-#pragma unroll
-            for (int w = 0; w < V; ++w) {
-                f32x4 z = b2r[w];
-#pragma unroll
-                for (int v = 0; v < V; ++v)
-                    if (!SP || ((coco_hop2_mask3(w) >> v) & 1u)) {
-                        const float av = __builtin_bit_cast(
-                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + w) / 64]), (v * V + w) % 64));
-                        z += av * accg[v];
-                    }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-                f16x4 h, l;
-                split4(z, h, l);
-                const int row = f * V + w;
-                *reinterpret_cast<f16x4*>(zb + sbo(row, uh)) = h;
-                *reinterpret_cast<f16x4*>(zb + sbo(row, 4 + uh)) = l;
+        issue_g(0, 0);
+        if (G::NKG > 1) issue_g(1, 1);
+    #pragma unroll
+        for (int kb = 0; kb < G::NKG; ++kb) {
+            if (kb + 1 < G::NKG) {   // chunk kb+1 may stay in flight
+                if (nxj == NXJ) wait_vm<NXJ + NWJ>();
+                else wait_vm<(NXJ > 0 ? NXJ - 1 : 0) + NWJ>();
+            } else {
+                wait_vm<0>();
             }
-        };
-        if (a.mix_sparse) mix_all(std::true_type{});
-        else mix_all(std::false_type{});
-    } else if (tid - 256 < G::NKB * 8) {   // zero rows (taps past a window edge)
-        const int i = tid - 256;
-        *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+            __builtin_amdgcn_s_barrier();
+            if (gw) {
+                const unsigned char* X = ring + (kb & 1) * G::GSLOT;
+                const unsigned char* W = X + G::XS;
+                const int r = wave * 16 + (lane & 15);
+                const f16x8 ah = *reinterpret_cast<const f16x8*>(W + sbo(r, g));
+                const f16x8 al = *reinterpret_cast<const f16x8*>(W + sbo(r, 4 + g));
+    #pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int rx = j * 16 + (lane & 15);
+                    const f16x8 bh = *reinterpret_cast<const f16x8*>(X + sbo(rx, g));
+                    const f16x8 bl = *reinterpret_cast<const f16x8*>(X + sbo(rx, 4 + g));
+                    accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, accg[j], 0, 0, 0);
+                    accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, accg[j], 0, 0, 0);
+                    accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, accg[j], 0, 0, 0);
+                }
+            }
+            if (kb + 2 < G::NKG) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                issue_g(kb + 2, kb & 1);
+            }
+        }
+        // bias2 of this lane's 4 channels for all joints: loaded before the Wt
+        // DMAs below so its wait does not queue behind them
+        const int mc = wave * 16 + 4 * g;   // mix channels mc .. mc+3 (waves 0-3)
+        f32x4 b2r[V];
+    #pragma unroll
+        for (int w = 0; w < V; ++w)
+            b2r[w] = gw ? *reinterpret_cast<const f32x4*>(a.bias2 + w * COUT + mc) : f32x4{0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (a.trace) tr[1] = __builtin_amdgcn_s_memrealtime();
+        // the ring is free: the first Wt chunks load during the mix
+    #pragma unroll
+        for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
+        if (a.trace) tr[2] = __builtin_amdgcn_s_memrealtime();
+
+        // ================= 2. mix in registers: z[w] = ReLU(bias2[w] + sum_v A[v][w] y[v])
+        if (gw) {
+            const int f = lane & 15, cc = mc & 31;
+            unsigned char* zb = zimg + (mc >> 5) * G::ZB + (cc & 4) * 2;
+            const int uh = cc >> 3;
+            auto mix_all = [&](auto sparse_tag) {
+                constexpr bool SP = decltype(sparse_tag)::value;
+    #pragma unroll
+                for (int w = 0; w < V; ++w) {
+                    f32x4 z = b2r[w];
+    #pragma unroll
+                    for (int v = 0; v < V; ++v)
+                        if (!SP || ((coco_hop2_mask3(w) >> v) & 1u)) {
+                            const float av = __builtin_bit_cast(
+                                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + w) / 64]), (v * V + w) % 64));
+                            z += av * accg[v];
+                        }
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                    f16x4 h, l;
+                    split4(z, h, l);
+                    const int row = f * V + w;
+                    *reinterpret_cast<f16x4*>(zb + sbo(row, uh)) = h;
+                    *reinterpret_cast<f16x4*>(zb + sbo(row, 4 + uh)) = l;
+                }
+            };
+            if (a.mix_sparse) mix_all(std::true_type{});
+            else mix_all(std::false_type{});
+        } else if (tid - 256 < G::NKB * 8) {   // zero rows (taps past a window edge)
+            const int i = tid - 256;
+            *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
 
     // ================= 3. T: out = z (*) Wt over 3 taps, A from the resident z image
     constexpr int NCGT = COUT / 64, WR = 8 / NCGT, NRB = (G::TRB + WR - 1) / WR;
@@ -283,11 +358,16 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     constexpr int C4 = COUT / 4, RS = 512 / C4, KI = (G::TR + RS - 1) / RS;
     const int c4 = tid % C4, lr0 = tid / C4, col = 4 * c4;
     f32x4 rr[KI];   // raw residual halves (hi dwords 0-1, lo 2-3), loaded before the staging
+    float rw[4][4];  // RAW: residual conv weights of this thread's 4 channels
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rw[e][c] = (RAW && c < a.c0) ? a.rw[(col + e) * a.c0 + c] : 0.f;
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
         rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int lr = lr0 + k * RS;
-        if (a.resid && lr < G::TR && r0 + lr < M) {
+        if (!RAW && a.resid && lr < G::TR && r0 + lr < M) {
             const unsigned short* rp = a.x + (size_t)(r0 + lr) * a.ldx + sbc(col);
             const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
             const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
@@ -315,12 +395,21 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
         const int lr = lr0 + k * RS, row = r0 + lr;
         if (lr >= G::TR || row >= M) continue;
         f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * G::LDC + col) + bv;
-        const f16x4 h = __builtin_bit_cast(f16x4, f32x2{rr[k][0], rr[k][1]});
-        const f16x4 l = __builtin_bit_cast(f16x4, f32x2{rr[k][2], rr[k][3]});
+        if constexpr (RAW) {   // 3 -> Cout residual conv of data_bn(x) (output frame = z image frame + 1)
+            const f32x4 xb = *reinterpret_cast<const f32x4*>(xsf + (lr + V) * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            v[e] += (float)h[e] + (float)l[e];
-            v[e] = v[e] > 0.f ? v[e] : 0.f;
+            for (int e = 0; e < 4; ++e) {
+                v[e] += xb[0] * rw[e][0] + xb[1] * rw[e][1] + xb[2] * rw[e][2] + xb[3] * rw[e][3];
+                v[e] = v[e] > 0.f ? v[e] : 0.f;
+            }
+        } else {
+            const f16x4 h = __builtin_bit_cast(f16x4, f32x2{rr[k][0], rr[k][1]});
+            const f16x4 l = __builtin_bit_cast(f16x4, f32x2{rr[k][2], rr[k][3]});
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] += (float)h[e] + (float)l[e];
+                v[e] = v[e] > 0.f ? v[e] : 0.f;
+            }
         }
         f16x4 oh, ol;
         split4(v, oh, ol);
@@ -352,6 +441,22 @@ hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st) {
     using G = StbGeo<64, 64, 16>;
     const int QO = a.nwin * a.T;
     hipLaunchKernelGGL((stblock_kernel<64, 64, 16>), dim3((QO + G::F - 1) / G::F), dim3(512), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_stblock0(const StbArgs& a, int cout, hipStream_t st) {
+    if (a.nwin <= 0 || a.T <= 0) return hipSuccess;
+    if (cout != 64 || !a.xraw || a.c0 < 1 || a.c0 > 4 || !a.bn_sc || !a.bn_sh || !a.wg0 || a.ldwg0 < a.c0 || !a.rw ||
+        !a.wt || !a.bias || !a.bias2 || !a.amix || !a.out)
+        return hipErrorInvalidValue;
+    if (a.ldo < 64 * (cout / 32) || a.ldo % 8 || a.ldwt < 3 * 64 * (cout / 32) || a.ldwt % 8)
+        return hipErrorInvalidValue;
+    StbArgs b = a;
+    b.x = nullptr; b.ldx = 64; b.wg = a.wt; b.ldwg = 64; b.resid = 0;   // unused by the raw G phase
+    (void)hipGetLastError();
+    using G = StbGeo<64, 64, 16>;
+    const int QO = a.nwin * a.T;
+    hipLaunchKernelGGL((stblock_kernel<64, 64, 16, true>), dim3((QO + G::F - 1) / G::F), dim3(512), 0, st, b);
     return hipGetLastError();
 }
 

@@ -29,7 +29,7 @@
 namespace tik {
 
 template <int BM, int BN, int WM, int WN, int NSA, int FG = 0>
-__global__ __launch_bounds__(64 * WM * WN) void tgemm_kernel(Cgemm3Args a) {
+__global__ __launch_bounds__(64 * WM * WN, WM * WN / 2) void tgemm_kernel(Cgemm3Args a) {
     constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
     constexpr int NW = WM * WN, NT = 64 * NW;
     static_assert(FM * WM * 16 == BM && FN * WN * 16 == BN, "tile");

@@ -390,7 +390,25 @@ struct Layer {
                         2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * (TK * cout + cin) * cout,
                         4.0 * (px_in * cin + px_out * cout + (double)TK * cout * cout), st);
             p.out(out, (size_t)rout * ldz * 2);
+            static const bool trace0 = getenv("TIK_STB_TRACE") != nullptr;   // debug: per-phase workgroup timing
+            const int nwg = (N * tin + 13) / 14;
+            unsigned long long* d = nullptr;
+            if (trace0) {
+                HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
+                b.trace = d;
+            }
             HIP_TRY(tik::launch_stblock0(b, cout, st));
+            if (trace0) {
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<unsigned long long> h((size_t)nwg * 6);
+                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipFree(d));
+                double ph[5] = {0, 0, 0, 0, 0};
+                for (int w = 0; w < nwg; ++w)
+                    for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
+                fprintf(stderr, "stblock0 L0 (%d wg): per-wg us G(raw) %.2f - %.2f wt-issue %.2f T %.2f epi %.2f\n", nwg,
+                        ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100, ph[4] / nwg / 100);
+            }
             return TIK_OK;
         }
         if (zready) {

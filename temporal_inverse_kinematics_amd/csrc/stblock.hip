@@ -134,7 +134,21 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
 
     float* const xsf = reinterpret_cast<float*>(smem + G::SMEM);
     if constexpr (RAW) {
-        // ================= 1'. G from the raw keypoints: data_bn(x) of the 16 frames -> LDS
+        // ================= 1'. G from the raw keypoints. Thread (frame f, channels
+        // co..co+3) of a joint half: waves 0-3 joints 0-8, waves 4-7 joints 9-16; every
+        // thread forms y for all 17 joints (the mix input), each half mixes its joints.
+        const int f = tid & 15, co = 4 * ((tid >> 4) & 15), half = wave >> 2;
+        const int w0 = half ? 9 : 0;
+        // weights and bias2' first: their latency overlaps the keypoint staging
+        float w[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? a.wg0[(co + e) * a.ldwg0 + c] : 0.f;
+        f32x4 b[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) b[k] = w0 + k < V ? *reinterpret_cast<const f32x4*>(a.bias2 + (w0 + k) * COUT + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+        // data_bn(x) of the 16 frames -> LDS
         for (int i = tid; i < FIN * V * 4; i += 512) {
             const int c = i & 3, p = i >> 2;
             const int v = p % V, fr = fi0 + p / V;
@@ -142,15 +156,10 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
             if (c < a.c0 && fr >= 0 && fr < QO) val = fmaf(a.xraw[((size_t)fr * V + v) * a.c0 + c], a.bn_sc[v * a.c0 + c], a.bn_sh[v * a.c0 + c]);
             xsf[i] = val;
         }
+        if (tid < G::NKB * 8)   // zero rows (taps past a window edge)
+            *reinterpret_cast<f32x4*>(zimg + (tid >> 3) * G::ZB + G::ZR * 128 + (tid & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
         __syncthreads();
-        if (tid < 256) {
-            // (frame f, channels co..co+3) x all 17 joints, the gcn0 arithmetic
-            const int f = tid & 15, co = 4 * (tid >> 4);
-            float w[4][4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? a.wg0[(co + e) * a.ldwg0 + c] : 0.f;
+        {
             f32x4 y[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
@@ -158,17 +167,15 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) y[v][e] = xp[0] * w[e][0] + xp[1] * w[e][1] + xp[2] * w[e][2] + xp[3] * w[e][3];
             }
-            f32x4 b[V];
-#pragma unroll
-            for (int wj = 0; wj < V; ++wj) b[wj] = *reinterpret_cast<const f32x4*>(a.bias2 + wj * COUT + co);
             const int cc = co & 31;
             unsigned char* zb = zimg + (co >> 5) * G::ZB + (cc & 4) * 2;
             const int uh = cc >> 3;
-            auto mix_all = [&](auto sparse_tag) {
+            auto mix_range = [&](auto w0c, auto w1c, auto sparse_tag) {
+                constexpr int W0 = decltype(w0c)::value, W1 = decltype(w1c)::value;
                 constexpr bool SP = decltype(sparse_tag)::value;
 #pragma unroll
-                for (int wj = 0; wj < V; ++wj) {
-                    f32x4 z = b[wj];
+                for (int wj = W0; wj < W1; ++wj) {
+                    f32x4 z = b[wj - W0];
 #pragma unroll
                     for (int v = 0; v < V; ++v)
                         if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
@@ -185,11 +192,16 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
                     *reinterpret_cast<f16x4*>(zb + sbo(row, 4 + uh)) = l;
                 }
             };
-            if (a.mix_sparse) mix_all(std::true_type{});
-            else mix_all(std::false_type{});
-        } else if (tid - 256 < G::NKB * 8) {   // zero rows (taps past a window edge)
-            const int i = tid - 256;
-            *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+            using I0 = std::integral_constant<int, 0>;
+            using I9 = std::integral_constant<int, 9>;
+            using I17 = std::integral_constant<int, 17>;
+            if (half) {
+                if (a.mix_sparse) mix_range(I9{}, I17{}, std::true_type{});
+                else mix_range(I9{}, I17{}, std::false_type{});
+            } else {
+                if (a.mix_sparse) mix_range(I0{}, I9{}, std::true_type{});
+                else mix_range(I0{}, I9{}, std::false_type{});
+            }
         }
         if (a.trace) tr[1] = tr[2] = __builtin_amdgcn_s_memrealtime();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -505,6 +505,17 @@ struct tik_model {
     SBW sb0, sb3;
     int prec = 1;
     DevBuf xb, z, z2, a0, a1, hid; // workspace (z, z2: ping-pong for the fused T+G launches)
+    // second workspace + private stream: large f16x3 batches run as two halves on
+    // two streams, so one half's launches fill the other's tails and epilogues
+    DevBuf xb_b, z_b, z2_b, a0_b, a1_b, hid_b;
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool split = true;                 // TIK_SPLIT=0: one stream
+    ~tik_model() {
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (aux) (void)hipStreamDestroy(aux);
+    }
     DevBuf part;                   // split-K partial sums (small-batch launches)
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
@@ -643,6 +654,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
     if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
+    if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
         else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
@@ -684,6 +696,35 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
     if ((rc = m->xb.reserve((size_t)N * T * V * 32)) || (rc = m->z.reserve(zmax)) || (rc = m->z2.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
         (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
         return rc;
+    return TIK_OK;
+}
+
+struct WsPtrs {
+    float *xb, *z, *z2, *a0, *a1, *hid;
+};
+static WsPtrs ws_of(tik_model* m, int k) {
+    return k == 0 ? WsPtrs{m->xb.p, m->z.p, m->z2.p, m->a0.p, m->a1.p, m->hid.p}
+                  : WsPtrs{m->xb_b.p, m->z_b.p, m->z2_b.p, m->a0_b.p, m->a1_b.p, m->hid_b.p};
+}
+// the second workspace set (split halves)
+static int reserve_b(tik_model* m, int N, int T) {
+    const size_t V = m->V;
+    size_t zmax = 0, amax = 0;
+    int t = T;
+    for (const Layer& L : m->layers) {
+        zmax = std::max(zmax, (size_t)N * t * V * L.cout);
+        t = Layer::tout(t, L.stride);
+        amax = std::max(amax, (size_t)N * t * V * L.cout);
+    }
+    int rc;
+    if ((rc = m->xb_b.reserve((size_t)N * T * V * 32)) || (rc = m->z_b.reserve(zmax)) || (rc = m->z2_b.reserve(zmax)) ||
+        (rc = m->a0_b.reserve(amax)) || (rc = m->a1_b.reserve(amax)) || (rc = m->hid_b.reserve((size_t)N * t * m->hidden)))
+        return rc;
+    if (!m->aux) {
+        HIP_TRY(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+    }
     return TIK_OK;
 }
 
@@ -734,9 +775,9 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
 // layer reads and writes SB rows, operands reach LDS by DMA. Returns the
 // features (SB rows of the last layer) and their row stride.
 static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t** feat_out, int* ld_out, int* tout,
-                     hipStream_t st) {
+                     hipStream_t st, const WsPtrs& w) {
     const int V = m->V;
-    half_t* xs = reinterpret_cast<half_t*>(m->xb.p);
+    half_t* xs = reinterpret_cast<half_t*>(w.xb);
     const long long px = (long long)N * T * V;
     if (!(m->layers.front().raw_ok() && m->layers.front().cin == m->C0)) {
         ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
@@ -744,9 +785,9 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
     }
     const half_t* cur = xs;
     int ld = 64, t = T, rc;
-    half_t* bufs[2] = {reinterpret_cast<half_t*>(m->a0.p), reinterpret_cast<half_t*>(m->a1.p)};
+    half_t* bufs[2] = {reinterpret_cast<half_t*>(w.a0), reinterpret_cast<half_t*>(w.a1)};
     int which = 0;
-    half_t* zb[2] = {reinterpret_cast<half_t*>(m->z.p), reinterpret_cast<half_t*>(m->z2.p)};
+    half_t* zb[2] = {reinterpret_cast<half_t*>(w.z), reinterpret_cast<half_t*>(w.z2)};
     int zi = 0;
     bool zready = false;
     for (size_t li = 0; li < m->layers.size(); ++li) {
@@ -756,7 +797,7 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
         const Layer* nxt = (m->fuse_tg && li + 1 < m->layers.size() && L.can_fuse_next(m->layers[li + 1]))
                                ? &m->layers[li + 1] : nullptr;
         if ((rc = L.forward3(cur, ld, N, t, zb[zi], o, m->zeros.p, st, false, raw ? x : nullptr, m->bn_sc.p,
-                             m->bn_sh.p, m->xb.p, m->stblock, nxt, zb[zi ^ 1], zready)))
+                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready)))
             return rc;
         zready = nxt != nullptr;
         if (nxt) zi ^= 1;
@@ -781,7 +822,7 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
             const int n = std::min(chunk, N - n0);
             const half_t* f;
             int ld;
-            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st))) return rc;
+            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st, ws_of(m, 0)))) return rc;
             const int C = m->layers.back().cout;
             HIP_TRY(tik::launch_merge(f, (long long)n * to * m->V, C, ld, feat + (size_t)n0 * to * m->feat, st));
         }
@@ -794,11 +835,11 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     return TIK_OK;
 }
 
-static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses, hipStream_t st) {
+static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses, hipStream_t st, const WsPtrs& w) {
     // the features of one frame are its V joint rows back to back: one SB row
     // of V * ldf halves whose blocks run over (joint, channel) = the reference
     // flatten order (st_gcn_aaai18.py:131-132)
-    half_t* hs = reinterpret_cast<half_t*>(m->hid.p);
+    half_t* hs = reinterpret_cast<half_t*>(w.hid);
     const int ldh = 64 * m->sb3.nblk;
     tik::Cgemm3Args h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
@@ -835,12 +876,34 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     if (use_dma(m, N, T)) {
         const int chunk = std::min(N, dma_chunk(m, T));
         if ((rc = tik_model_reserve(m, chunk, T))) return rc;
+        // two halves on two streams when the batch is large (not while profiling:
+        // per-launch events would time overlapping kernels)
+        const bool split = m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
+        if (split && (rc = reserve_b(m, (std::min(N, chunk) + 1) / 2, T))) return rc;
+        auto half = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w) -> int {
+            const half_t* fs;
+            int ld, r;
+            if ((r = backbone3(m, xs, n, T, &fs, &ld, &to, s, w))) return r;
+            return head3(m, fs, ld, n * to, ps, s, w);
+        };
         for (int n0 = 0; n0 < N; n0 += chunk) {
             const int n = std::min(chunk, N - n0);
-            const half_t* fs;
-            int ld;
-            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &fs, &ld, &to, st))) return rc;
-            if ((rc = head3(m, fs, ld, n * to, poses + (size_t)n0 * to * m->pose_dim, st))) return rc;
+            const float* xs = x + (size_t)n0 * T * m->V * m->C0;
+            const int To = tik_model_out_frames(m, T);
+            float* ps = poses + (size_t)n0 * To * m->pose_dim;
+            if (split && n >= 2 && (long long)n * T >= 32768) {
+                const int na = n / 2, nb = n - na;
+                HIP_TRY(hipEventRecord(m->ev_fork, st));
+                HIP_TRY(hipStreamWaitEvent(m->aux, m->ev_fork, 0));
+                if ((rc = half(xs, na, ps, st, ws_of(m, 0)))) return rc;
+                if ((rc = half(xs + (size_t)na * T * m->V * m->C0, nb, ps + (size_t)na * To * m->pose_dim, m->aux,
+                               ws_of(m, 1))))
+                    return rc;
+                HIP_TRY(hipEventRecord(m->ev_join, m->aux));
+                HIP_TRY(hipStreamWaitEvent(st, m->ev_join, 0));
+            } else if ((rc = half(xs, n, ps, st, ws_of(m, 0)))) {
+                return rc;
+            }
         }
         return TIK_OK;
     }

@@ -230,3 +230,23 @@ def test_fused_gcn_epilogue_bitwise():
         x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n)).cuda()
         with torch.no_grad():
             assert torch.equal(fused(x)["poses"], plain(x)["poses"]), (n, T)
+
+
+def test_two_stream_split_bitwise():
+    """Large f16x3 batches run as two halves on two HIP streams (second
+    workspace, fork/join events): poses bit-identical to the one-stream run,
+    including an odd batch and one the DMA sub-batching also splits."""
+    import os
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    split = synthetic_model(win_size=64, device="cuda").regressor
+    os.environ["TIK_SPLIT"] = "0"
+    try:
+        one = synthetic_model(win_size=64, device="cuda").regressor
+        one.tik_handle()
+    finally:
+        del os.environ["TIK_SPLIT"]
+    for n in (1024, 1001, 513):
+        x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 1)).cuda()
+        with torch.no_grad():
+            assert torch.equal(split(x)["poses"], one(x)["poses"]), n

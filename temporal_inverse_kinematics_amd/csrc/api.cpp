@@ -518,7 +518,8 @@ struct tik_model {
     }
     DevBuf part;                   // split-K partial sums (small-batch launches)
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
-    long long dma_min_frames = 4096;   // f16x3: N*T at or above -> split-activation DMA path
+    long long dma_min_frames = 1;      // f16x3: N*T at or above -> split-activation DMA path (TIK_GEMM_PATH)
+    int small_head_rows = 256;         // DMA path: output rows at or below -> split-K head (TIK_SMALL_HEAD)
     int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
     bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
     bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
@@ -655,6 +656,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
+    if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
         else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
@@ -867,6 +869,34 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
     return TIK_OK;
 }
 
+// Head on fp32 features with split-K (few rows: the K = 4352 loop spread over
+// workgroups instead of run serially by the handful of row tiles).
+static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, hipStream_t st) {
+    tik::CgemmArgs h{};
+    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
+    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
+    h.nseg = 1; h.bias = m->b0.p; h.out = hid; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
+    h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
+    h.partial = m->part.p;
+    {
+        ProfScope pr("H64x64.head0", 2.0 * rows * m->feat * m->hidden,
+                     4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
+        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x64, st, m->prec));
+    }
+    tik::CgemmArgs p{};
+    p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
+    p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
+    p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
+    p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
+    p.partial = m->part.p;
+    {
+        ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
+                     4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
+        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x64, st, m->prec));
+    }
+    return TIK_OK;
+}
+
 int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream) {
     if (!m || !x || !poses || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: bad arguments");
     hipStream_t st = (hipStream_t)stream;
@@ -884,6 +914,12 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
             const half_t* fs;
             int ld, r;
             if ((r = backbone3(m, xs, n, T, &fs, &ld, &to, s, w))) return r;
+            if ((long long)n * to <= m->small_head_rows && s == st) {
+                // few rows (online IK): features to fp32 in the free ping-pong buffer, split-K head
+                float* ff = reinterpret_cast<const float*>(fs) == w.a0 ? w.a1 : w.a0;
+                HIP_TRY(tik::launch_merge(fs, (long long)n * to * m->V, m->layers.back().cout, ld, ff, s));
+                return head_splitk(m, ff, n * to, ps, w.hid, s);
+            }
             return head3(m, fs, ld, n * to, ps, s, w);
         };
         for (int n0 = 0; n0 < N; n0 += chunk) {
@@ -909,30 +945,7 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
     }
     if ((rc = tik_model_reserve(m, N, T))) return rc;
     if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
-    const int rows = N * to;
-    tik::CgemmArgs h{};
-    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
-    h.nseg = 1; h.bias = m->b0.p; h.out = m->hid.p; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
-    h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
-    h.partial = m->part.p;
-    {
-        ProfScope pr("H64x64.head0", 2.0 * rows * m->feat * m->hidden,
-                     4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
-        HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x64, st, m->prec));
-    }
-    tik::CgemmArgs p{};
-    p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = mkseg(m->hid.p, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
-    p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
-    p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
-    p.partial = m->part.p;
-    {
-        ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
-                     4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
-        HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x64, st, m->prec));
-    }
-    return TIK_OK;
+    return head_splitk(m, f, N * to, poses, m->hid.p, st);
 }
 
 int tik_model_set_precision(tik_model_t m, int prec) {

@@ -14,11 +14,11 @@ TOL = 1e-4
 
 
 @pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
-                                                 "f16x3-layered", "f16x3-nofuse"])
+                                                 "f16x3-layered", "f16x3-nofuse", "f16x3-dmahead"])
 def model(request):
-    """fp32 MFMA; f16x3 with the size-based choice of GEMM path (register-staged
-    fp32 activations + split-K for small batches, split-plane activations with
-    LDS DMA for large ones); and each f16x3 path forced at every size."""
+    """fp32 MFMA; f16x3 with the default GEMM path (split-block activations with
+    LDS DMA at every size, the head as a split-K GEMM on fp32 features when it
+    has few rows); and each f16x3 path forced at every size."""
     import os
     from temporal_inverse_kinematics_amd import _build
     _build.build()
@@ -30,10 +30,12 @@ def model(request):
         # 2 GiB-per-tensor split of large batches, exercised at test sizes);
         # "layered": the DMA path with every block as separate G and T kernels
         # (no whole-block stblock kernel); "nofuse": the DMA path without the next
-        # block's gcn fused into the temporal-conv epilogue (separate G launches)
+        # block's gcn fused into the temporal-conv epilogue (separate G launches);
+        # "dmahead": the DMA path with the split-block head GEMMs at every size
         env = {"dmachunk": {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"},
                "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"},
-               "nofuse": {"TIK_GEMM_PATH": "dma", "TIK_FUSE_TG": "0"}}.get(path, {"TIK_GEMM_PATH": path})
+               "nofuse": {"TIK_GEMM_PATH": "dma", "TIK_FUSE_TG": "0"},
+               "dmahead": {"TIK_GEMM_PATH": "dma", "TIK_SMALL_HEAD": "0"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created

@@ -264,6 +264,22 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN / 2) void tgemm_kernel(Cgemm3
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (a.trace) tp[0] = __builtin_amdgcn_s_memrealtime();
+        // B operand of the next gcn: its SB weights (L2-resident) for this wave's
+        // columns, in two halves of K issued ahead of the work that hides them
+        // (the first here, over the residual wait; the second over the image store)
+        f16x8 gh[NKB][FN], gl[NKB][FN];
+        auto load_g = [&](int kb0, int kb1) {
+#pragma unroll
+            for (int kb = kb0; kb < kb1; ++kb)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const unsigned short* p = a.g_w + (size_t)(brow + j * 16) * a.g_ldw + kb * 64 + 8 * g;
+                    gh[kb][j] = *reinterpret_cast<const f16x8*>(p);
+                    gl[kb][j] = *reinterpret_cast<const f16x8*>(p + 32);
+                }
+        };
+        load_g(0, NKB / 2);
+        __builtin_amdgcn_sched_barrier(0);
         // (2) this thread's output items
         const int c4 = tid % E::C4, lr0 = tid / E::C4, col = 4 * c4;
         const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
@@ -282,6 +298,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN / 2) void tgemm_kernel(Cgemm3
             const bool ok = lr < RT && r0 + lr < a.M;
             vv[k] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        load_g(NKB / 2, NKB);
+        __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();   // every C read done: the image goes over it
         // (3) the split image (zero rows past the tile's frames)
@@ -297,16 +315,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN / 2) void tgemm_kernel(Cgemm3
                 *reinterpret_cast<f16x4*>(ib + sbo(lr, 4 + uh) + sub) = l;
             }
         }
-        // B operand of the next gcn: its SB weights (L2-resident) for this wave's columns
-        f16x8 gh[NKB][FN], gl[NKB][FN];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const unsigned short* p = a.g_w + (size_t)(brow + j * 16) * a.g_ldw + kb * 64 + 8 * g;
-                gh[kb][j] = *reinterpret_cast<const f16x8*>(p);
-                gl[kb][j] = *reinterpret_cast<const f16x8*>(p + 32);
-            }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (a.trace) tp[1] = __builtin_amdgcn_s_memrealtime();

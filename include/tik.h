@@ -6,8 +6,12 @@
  * legacy default stream), is stream-ordered, and returns an int status:
  * TIK_OK (0) or a negative TIK_E_* code; tik_last_error() returns the text of
  * the calling thread's last failure. Handles own their device weights and
- * workspace; per-call functions allocate only through the handle. Calls are
- * thread-safe across distinct handles/streams.
+ * workspace; per-call functions allocate only through the handle. One
+ * handle serves one stream at a time: calls on the same handle must be
+ * stream-ordered (they share its workspace, which a call may grow). Distinct
+ * handles are independent. An online-IK stream (tik_stream_*) owns its own
+ * workspace and a reference on its model, so it may run concurrently with
+ * batch calls on that model's handle, and outlives tik_model_destroy.
  *
  * Each entry point names the reference interface it replaces
  * (paths relative to the reference repository root).
@@ -141,6 +145,9 @@ int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h
  * 0 before, <0 on error. The step is one hipGraph replay when use_graph != 0.
  * Flush the last h frames by pushing the last frame h more times.
  * ---------------------------------------------------------------------- */
+/* The stream keeps a reference on `model` (released by tik_stream_destroy)
+ * and a private workspace sized for (1, 2h+1): batch calls on the model handle
+ * (any size, any stream) do not disturb a live stream. */
 typedef struct tik_stream* tik_stream_t;
 int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream_t* out);
 int tik_stream_destroy(tik_stream_t s);

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -504,19 +505,20 @@ struct tik_model {
     SplitW sw0, sw3;
     SBW sb0, sb3;
     int prec = 1;
-    DevBuf xb, z, z2, a0, a1, hid; // workspace (z, z2: ping-pong for the fused T+G launches)
-    // second workspace + private stream: large f16x3 batches run as two halves on
-    // two streams, so one half's launches fill the other's tails and epilogues
-    DevBuf xb_b, z_b, z2_b, a0_b, a1_b, hid_b;
+    // ws[0]: the handle's workspace (z, z2: ping-pong for the fused T+G launches);
+    // ws[1] + a private stream: large f16x3 batches run as two halves on two
+    // streams, so one half's launches fill the other's tails and epilogues.
+    // Online-IK streams own their workspaces (stream.cpp).
+    Workspace ws[2];
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool split = true;                 // TIK_SPLIT=0: one stream
+    std::atomic<int> refs{1};          // the handle + every live online-IK stream
     ~tik_model() {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
         if (aux) (void)hipStreamDestroy(aux);
     }
-    DevBuf part;                   // split-K partial sums (small-batch launches)
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 1;      // f16x3: N*T at or above -> split-activation DMA path (TIK_GEMM_PATH)
     int small_head_rows = 256;         // DMA path: output rows at or below -> split-K head (TIK_SMALL_HEAD)
@@ -647,8 +649,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
     md->prec = default_precision();
-    // split-K workspace: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
-    if ((rc = md->part.reserve((size_t)384 * 128 * 128)) || (rc = md->zeros.upload(std::vector<unsigned short>(64, 0)))) {
+    if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0)))) {
         delete md;
         return rc;
     }
@@ -674,7 +675,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
 }
 
 int tik_model_destroy(tik_model_t m) {
-    delete m;
+    if (m) model_release(m);   // freed now, or when its last online-IK stream is destroyed
     return TIK_OK;
 }
 
@@ -684,8 +685,10 @@ int tik_model_out_frames(tik_model_t m, int T) {
     return T;
 }
 
-int tik_model_reserve(tik_model_t m, int N, int T) {
-    if (!m || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_model_reserve: bad arguments");
+}  // extern "C"
+
+namespace tik_host {
+int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
     const size_t V = m->V;
     size_t zmax = 0, amax = 0;
     int t = T;
@@ -695,33 +698,35 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
     int rc;
-    if ((rc = m->xb.reserve((size_t)N * T * V * 32)) || (rc = m->z.reserve(zmax)) || (rc = m->z2.reserve(zmax)) || (rc = m->a0.reserve(amax)) ||
-        (rc = m->a1.reserve(amax)) || (rc = m->hid.reserve((size_t)N * t * m->hidden)))
+    // split-K partials: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
+    if ((rc = w.xb.reserve((size_t)N * T * V * 32)) || (rc = w.z.reserve(zmax)) || (rc = w.z2.reserve(zmax)) ||
+        (rc = w.a0.reserve(amax)) || (rc = w.a1.reserve(amax)) || (rc = w.hid.reserve((size_t)N * t * m->hidden)) ||
+        (rc = w.part.reserve((size_t)384 * 128 * 128)))
         return rc;
     return TIK_OK;
 }
 
-struct WsPtrs {
-    float *xb, *z, *z2, *a0, *a1, *hid;
-};
-static WsPtrs ws_of(tik_model* m, int k) {
-    return k == 0 ? WsPtrs{m->xb.p, m->z.p, m->z2.p, m->a0.p, m->a1.p, m->hid.p}
-                  : WsPtrs{m->xb_b.p, m->z_b.p, m->z2_b.p, m->a0_b.p, m->a1_b.p, m->hid_b.p};
+void model_retain(tik_model* m) { m->refs.fetch_add(1); }
+void model_release(tik_model* m) {
+    if (m->refs.fetch_sub(1) == 1) delete m;
 }
-// the second workspace set (split halves)
+}  // namespace tik_host
+
+extern "C" {
+
+int tik_model_reserve(tik_model_t m, int N, int T) {
+    if (!m || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_model_reserve: bad arguments");
+    return model_reserve_ws(m, m->ws[0], N, T);
+}
+
+struct WsPtrs {
+    float *xb, *z, *z2, *a0, *a1, *hid, *part;
+};
+static WsPtrs ptrs_of(const Workspace& w) { return WsPtrs{w.xb.p, w.z.p, w.z2.p, w.a0.p, w.a1.p, w.hid.p, w.part.p}; }
+// the second workspace set (split halves) and the aux stream
 static int reserve_b(tik_model* m, int N, int T) {
-    const size_t V = m->V;
-    size_t zmax = 0, amax = 0;
-    int t = T;
-    for (const Layer& L : m->layers) {
-        zmax = std::max(zmax, (size_t)N * t * V * L.cout);
-        t = Layer::tout(t, L.stride);
-        amax = std::max(amax, (size_t)N * t * V * L.cout);
-    }
     int rc;
-    if ((rc = m->xb_b.reserve((size_t)N * T * V * 32)) || (rc = m->z_b.reserve(zmax)) || (rc = m->z2_b.reserve(zmax)) ||
-        (rc = m->a0_b.reserve(amax)) || (rc = m->a1_b.reserve(amax)) || (rc = m->hid_b.reserve((size_t)N * t * m->hidden)))
-        return rc;
+    if ((rc = model_reserve_ws(m, m->ws[1], N, T))) return rc;
     if (!m->aux) {
         HIP_TRY(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
@@ -752,20 +757,21 @@ static int dma_chunk(const tik_model* m, int T) {
 }
 
 // Backbone on fp32 activations (both precisions; split-K for small batches).
-static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st) {
+static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st,
+                    const WsPtrs& w) {
     const int V = m->V;
     {
         const double px = (double)N * T * V;
         ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
-        HIP_TRY(tik::launch_data_bn(x, N * T * V, V, m->C0, m->bn_sc.p, m->bn_sh.p, m->xb.p, st));
+        HIP_TRY(tik::launch_data_bn(x, N * T * V, V, m->C0, m->bn_sc.p, m->bn_sh.p, w.xb, st));
     }
-    const float* cur = m->xb.p;
+    const float* cur = w.xb;
     int ld = 4, t = T, rc;
-    float* bufs[2] = {m->a0.p, m->a1.p};
+    float* bufs[2] = {w.a0, w.a1};
     int which = 0;
     for (const Layer& L : m->layers) {
         float* o = bufs[which];
-        if ((rc = L.forward(cur, ld, N, t, m->z.p, o, st, m->prec, m->part.p))) return rc;
+        if ((rc = L.forward(cur, ld, N, t, w.z, o, st, m->prec, w.part))) return rc;
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);
@@ -824,7 +830,8 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
             const int n = std::min(chunk, N - n0);
             const half_t* f;
             int ld;
-            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st, ws_of(m, 0)))) return rc;
+            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st, ptrs_of(m->ws[0]))))
+                return rc;
             const int C = m->layers.back().cout;
             HIP_TRY(tik::launch_merge(f, (long long)n * to * m->V, C, ld, feat + (size_t)n0 * to * m->feat, st));
         }
@@ -832,7 +839,7 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     }
     if ((rc = tik_model_reserve(m, N, T))) return rc;
     float* f;
-    if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
+    if ((rc = backbone(m, x, N, T, &f, &to, st, ptrs_of(m->ws[0])))) return rc;
     HIP_TRY(hipMemcpyAsync(feat, f, sizeof(float) * (size_t)N * to * m->feat, hipMemcpyDeviceToDevice, st));
     return TIK_OK;
 }
@@ -871,13 +878,13 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
 
 // Head on fp32 features with split-K (few rows: the K = 4352 loop spread over
 // workgroups instead of run serially by the handful of row tiles).
-static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, hipStream_t st) {
+static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, float* part, hipStream_t st) {
     tik::CgemmArgs h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
     h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = hid; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
     h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
-    h.partial = m->part.p;
+    h.partial = part;
     {
         ProfScope pr("H64x64.head0", 2.0 * rows * m->feat * m->hidden,
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
@@ -888,7 +895,7 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
     p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
     p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
-    p.partial = m->part.p;
+    p.partial = part;
     {
         ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
                      4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
@@ -897,18 +904,19 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
     return TIK_OK;
 }
 
-int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream) {
-    if (!m || !x || !poses || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: bad arguments");
-    hipStream_t st = (hipStream_t)stream;
-    ProfGuard pg(m);
+}  // extern "C"
+
+namespace tik_host {
+int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, hipStream_t st, Workspace& ws,
+                     bool allow_split) {
     float* f;
     int to, rc;
     if (use_dma(m, N, T)) {
         const int chunk = std::min(N, dma_chunk(m, T));
-        if ((rc = tik_model_reserve(m, chunk, T))) return rc;
+        if ((rc = model_reserve_ws(m, ws, chunk, T))) return rc;
         // two halves on two streams when the batch is large (not while profiling:
         // per-launch events would time overlapping kernels)
-        const bool split = m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
+        const bool split = allow_split && m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
         if (split && (rc = reserve_b(m, (std::min(N, chunk) + 1) / 2, T))) return rc;
         auto half = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w) -> int {
             const half_t* fs;
@@ -918,7 +926,7 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
                 // few rows (online IK): features to fp32 in the free ping-pong buffer, split-K head
                 float* ff = reinterpret_cast<const float*>(fs) == w.a0 ? w.a1 : w.a0;
                 HIP_TRY(tik::launch_merge(fs, (long long)n * to * m->V, m->layers.back().cout, ld, ff, s));
-                return head_splitk(m, ff, n * to, ps, w.hid, s);
+                return head_splitk(m, ff, n * to, ps, w.hid, w.part, s);
             }
             return head3(m, fs, ld, n * to, ps, s, w);
         };
@@ -931,21 +939,31 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
                 const int na = n / 2, nb = n - na;
                 HIP_TRY(hipEventRecord(m->ev_fork, st));
                 HIP_TRY(hipStreamWaitEvent(m->aux, m->ev_fork, 0));
-                if ((rc = half(xs, na, ps, st, ws_of(m, 0)))) return rc;
+                if ((rc = half(xs, na, ps, st, ptrs_of(ws)))) return rc;
                 if ((rc = half(xs + (size_t)na * T * m->V * m->C0, nb, ps + (size_t)na * To * m->pose_dim, m->aux,
-                               ws_of(m, 1))))
+                               ptrs_of(m->ws[1]))))
                     return rc;
                 HIP_TRY(hipEventRecord(m->ev_join, m->aux));
                 HIP_TRY(hipStreamWaitEvent(st, m->ev_join, 0));
-            } else if ((rc = half(xs, n, ps, st, ws_of(m, 0)))) {
+            } else if ((rc = half(xs, n, ps, st, ptrs_of(ws)))) {
                 return rc;
             }
         }
         return TIK_OK;
     }
-    if ((rc = tik_model_reserve(m, N, T))) return rc;
-    if ((rc = backbone(m, x, N, T, &f, &to, st))) return rc;
-    return head_splitk(m, f, N * to, poses, m->hid.p, st);
+    if ((rc = model_reserve_ws(m, ws, N, T))) return rc;
+    const WsPtrs w = ptrs_of(ws);
+    if ((rc = backbone(m, x, N, T, &f, &to, st, w))) return rc;
+    return head_splitk(m, f, N * to, poses, w.hid, w.part, st);
+}
+}  // namespace tik_host
+
+extern "C" {
+
+int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream) {
+    if (!m || !x || !poses || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: bad arguments");
+    ProfGuard pg(m);
+    return model_forward_ws(m, x, N, T, poses, (hipStream_t)stream, m->ws[0], true);
 }
 
 int tik_model_set_precision(tik_model_t m, int prec) {

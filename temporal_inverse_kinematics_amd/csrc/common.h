@@ -186,5 +186,26 @@ inline int default_precision() {
     return (e && (std::string(e) == "fp32" || std::string(e) == "f32")) ? 0 : 1;
 }
 
+// One set of activation buffers for the IK forward. A model handle owns two
+// (the caller-stream half and the aux-stream half of a split batch); every
+// online-IK stream owns its own, so a batch call on the handle can never
+// reallocate or overwrite memory a captured stream graph points at.
+struct Workspace {
+    DevBuf xb, z, z2, a0, a1, hid;   // input block, z ping-pong, activation ping-pong, head hidden
+    DevBuf part;                     // split-K partial sums (small-batch launches)
+};
+
+}  // namespace tik_host
+
+struct tik_model;
+namespace tik_host {
+// internal entry points shared by api.cpp and stream.cpp
+int model_reserve_ws(tik_model* m, Workspace& w, int N, int T);
+// the IK forward on workspace w; split = may run as two halves on two streams
+int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, hipStream_t st, Workspace& w,
+                     bool split);
+void model_retain(tik_model* m);    // a stream keeps its model alive
+void model_release(tik_model* m);   // deletes the model at the last reference
+
 
 }  // namespace tik_host

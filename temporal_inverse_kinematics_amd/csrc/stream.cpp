@@ -19,7 +19,8 @@
 using namespace tik_host;
 
 struct tik_stream {
-    tik_model_t model = nullptr;
+    tik_model_t model = nullptr;   // retained: the handle may be destroyed first
+    Workspace ws;                  // private: batch calls on the handle never touch it
     int h = 0, W = 0, V = 17, tout = 0, pose_dim = 66;
     hipStream_t st = nullptr;
     hipGraph_t graph = nullptr;
@@ -30,11 +31,13 @@ struct tik_stream {
     float* host_pose = nullptr;    // pinned
     long long pushed = 0;
     ~tik_stream() {
+        if (st) (void)hipStreamSynchronize(st);
         if (exec) (void)hipGraphExecDestroy(exec);
         if (graph) (void)hipGraphDestroy(graph);
         if (host_frame) (void)hipHostFree(host_frame);
         if (host_pose) (void)hipHostFree(host_pose);
         if (st) (void)hipStreamDestroy(st);
+        if (model) model_release(model);
     }
 };
 
@@ -42,7 +45,7 @@ static int record_step(tik_stream* s) {
     HIP_TRY(hipMemcpyAsync(s->frame_in.p, s->host_frame, sizeof(float) * s->V * 3, hipMemcpyHostToDevice, s->st));
     HIP_TRY(tik::launch_stream_push(s->ring.p, s->W, s->V * 3, s->count.p, s->frame_in.p, s->st));
     HIP_TRY(tik::launch_stream_window(s->ring.p, s->W, s->V, s->count.p, s->h, 11, 12, 1, s->window.p, s->st));
-    int rc = tik_ik_forward(s->model, s->window.p, 1, s->W, s->poses.p, s->st);
+    int rc = model_forward_ws(s->model, s->window.p, 1, s->W, s->poses.p, s->st, s->ws, false);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(s->host_pose, s->poses.p, sizeof(float) * s->pose_dim, hipMemcpyDeviceToHost, s->st));
     return TIK_OK;
@@ -54,12 +57,13 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
     if (!model || win_size <= 0 || !out) return fail(TIK_E_INVALID, "tik_stream_create: bad arguments");
     *out = nullptr;
     auto* s = new tik_stream();
+    model_retain(model);
     s->model = model;
     s->h = win_size / 2;
     s->W = 2 * s->h + 1;
     s->tout = tik_model_out_frames(model, s->W);
     int rc = 0;
-    if (s->tout <= 0 || (rc = tik_model_reserve(model, 1, s->W)) || (rc = s->ring.reserve((size_t)s->W * s->V * 3)) ||
+    if (s->tout <= 0 || (rc = model_reserve_ws(model, s->ws, 1, s->W)) || (rc = s->ring.reserve((size_t)s->W * s->V * 3)) ||
         (rc = s->window.reserve((size_t)s->W * s->V * 3)) || (rc = s->poses.reserve((size_t)s->tout * s->pose_dim)) ||
         (rc = s->frame_in.reserve((size_t)s->V * 3)) || (rc = s->count.reserve(1))) {
         delete s;

@@ -38,8 +38,10 @@ def sharded_forward(forward: Callable[[torch.Tensor], torch.Tensor], windows: to
     """Run `forward` on this rank's contiguous shard of `windows` (global batch,
     identical on every rank) and all-gather the results in global order.
     Uneven shards are padded to the largest shard for the collective and
-    trimmed afterwards."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    trimmed afterwards. A rank whose shard is empty (fewer windows than
+    ranks) still joins the collective: `forward` must map an empty batch to
+    an empty (0, ...) result, as PoseRegressor.forward does."""
+    if not dist.is_initialized() or dist.get_world_size() == 1 or windows.shape[0] == 0:
         return forward(windows)
     world, rank = dist.get_world_size(), dist.get_rank()
     n = windows.shape[0]

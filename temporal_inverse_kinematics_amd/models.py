@@ -216,13 +216,15 @@ class PoseRegressor(nn.Module):
         return self._tik.h
 
     def forward(self, x, init_pose=None, n_iter=3):
-        h = self.tik_handle()
-        x = x.contiguous()
-        _lib.require_gpu(x)
         if x.dim() != 4:
             raise ValueError(f"expected (N,T,V,C) keypoints, got shape {tuple(x.shape)}")
         N, T, V, C = x.shape
         To = self.backbone.out_frames(T)
+        if N == 0:   # an empty batch (e.g. an empty rank shard): empty poses, as torch would give
+            return {"poses": torch.empty((0, To, self.pose_dim), device=x.device, dtype=torch.float32)}
+        h = self.tik_handle()
+        x = x.contiguous()
+        _lib.require_gpu(x)
         poses = torch.empty((N, To, self.pose_dim), device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().tik_ik_forward(h, x.data_ptr(), N, T, poses.data_ptr(), _lib.stream_of(x)),
                    "PoseRegressor")
@@ -230,11 +232,13 @@ class PoseRegressor(nn.Module):
 
     def backbone_features(self, x):
         """StgGcn18.forward output (N,T',17*256) through the fused path."""
+        N, T = x.shape[:2]
+        To = self.backbone.out_frames(T)
+        if N == 0:
+            return torch.empty((0, To, 17 * 256), device=x.device, dtype=torch.float32)
         h = self.tik_handle()
         x = x.contiguous()
         _lib.require_gpu(x)
-        N, T = x.shape[:2]
-        To = self.backbone.out_frames(T)
         feat = torch.empty((N, To, 17 * 256), device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().tik_backbone_forward(h, x.data_ptr(), N, T, feat.data_ptr(), _lib.stream_of(x)),
                    "StgGcn18")

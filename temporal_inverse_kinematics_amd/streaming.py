@@ -24,6 +24,11 @@ class OnlineIK:
         self._model = model
         lib = _lib.load()
         handle = reg.tik_handle()
+        # the stream owns its workspace and holds a library reference on the
+        # model handle, so later batch calls (which may grow the handle's
+        # workspace) or a handle rebuilt after a weight change leave it intact;
+        # the Python reference below only documents that ownership
+        self._handle_ref = reg._tik
         s = _lib.ctypes.c_void_p()
         _lib.check(lib.tik_stream_create(handle, self.win_size, int(use_graph), _lib.ctypes.byref(s)), "OnlineIK")
         self._s = s.value

@@ -26,6 +26,7 @@ def _worker(rank, world, port, n, q):
     seen = []
 
     def fwd(x):
+        # PoseRegressor.forward's shape contract: (N,...) -> (N,...), N == 0 included
         seen.append(x.shape[0])
         return x * 2 + 1
 
@@ -42,7 +43,7 @@ def _worker(rank, world, port, n, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [8, 7])
+@pytest.mark.parametrize("n", [8, 7, 1])
 def test_sharded_gather_gloo_ws2(n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -63,3 +64,46 @@ def test_shard_range_covers():
             spans = [shard_range(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def _worker_model(rank, world, port, q):
+    """n < world with the real PoseRegressor: the rank with the empty shard
+    gets an empty (0,T',66) result from forward (no library call) and still
+    joins the all-gather; the other rank's forward is stubbed on CPU."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from temporal_inverse_kinematics_amd.distributed import sharded_forward
+    from temporal_inverse_kinematics_amd.models import PoseRegressor, default_hparams
+    m = PoseRegressor(default_hparams(win_size=64)).eval()
+    x = torch.zeros((1, 64, 17, 3))
+
+    def fwd(xs):
+        if xs.shape[0] == 0:
+            return m(xs)["poses"]
+        return torch.full((xs.shape[0], m.backbone.out_frames(64), 66), 7.0)
+
+    out = sharded_forward(fwd, x)
+    q.put((rank, tuple(out.shape) == (1, 4, 66) and bool((out == 7.0).all())))
+    dist.destroy_process_group()
+
+
+def test_empty_shard_joins_gather_gloo_ws2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_model, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: True, 1: True}
+
+
+def test_empty_batch_forward_cpu():
+    from temporal_inverse_kinematics_amd.models import PoseRegressor, default_hparams
+    m = PoseRegressor(default_hparams(win_size=64)).eval()
+    y = m(torch.zeros((0, 64, 17, 3)))["poses"]
+    assert tuple(y.shape) == (0, 4, 66)
+    f = m.backbone_features(torch.zeros((0, 9, 17, 3)))
+    assert tuple(f.shape) == (0, 1, 17 * 256)

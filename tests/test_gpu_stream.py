@@ -26,3 +26,47 @@ def test_stream_matches_run_inference(win, graph):
     # a second pass after reset gives the same answer
     again = online.run(seq)
     assert np.array_equal(again, got)
+
+
+def test_stream_survives_batch_calls_and_rebuilds():
+    """a live OnlineIK must not share the handle's workspace.
+    Create the stream FIRST, then run batch calls on the same model that grow
+    the handle's workspace (and run on another torch stream), then rebuild the
+    handle by changing a weight: the stream keeps giving the poses of the
+    weights it was created with, and its graph never touches freed memory."""
+    import torch
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import run_inference, synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    r = golden("run_inference.npz")
+    seq = r["seq"][:60]
+    m = synthetic_model(win_size=9, device="cuda")
+    online = OnlineIK(m, use_graph=True)
+    first = online.run(seq)
+    ref = run_inference(m, seq)
+    assert np.abs(first - ref).max() < 1e-5
+    # large batches on the handle: its workspace is reallocated several times,
+    # one of them on a non-default torch stream while the online stream is idle
+    x = torch.from_numpy(syn.synthetic_windows(700, 64, seed=3)).cuda()
+    with torch.no_grad():
+        m(x)
+        s2 = torch.cuda.Stream()
+        with torch.cuda.stream(s2):
+            m(torch.from_numpy(syn.synthetic_windows(1500, 64, seed=4)).cuda())
+        torch.cuda.synchronize()
+    assert np.array_equal(online.run(seq), first)
+    # a weight change rebuilds the handle (the old one is released); the
+    # stream still holds the old model and still reproduces its poses
+    with torch.no_grad():
+        m.regressor.pose_regressor[3].bias.add_(1.0)
+    moved = run_inference(m, seq)
+    assert np.abs(moved - ref).max() > 0.5
+    import gc
+    gc.collect()
+    assert np.array_equal(online.run(seq), first)
+    # a new stream follows the new weights
+    assert np.abs(OnlineIK(m, use_graph=True).run(seq) - moved).max() < 1e-5
+    del online
+    gc.collect()

@@ -330,7 +330,7 @@ struct Layer {
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
                  bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
                  const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true, const Layer* nxt = nullptr,
-                 half_t* znext = nullptr, bool zready = false) const {
+                 half_t* znext = nullptr, bool zready = false, half_t* trash = nullptr) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -455,6 +455,42 @@ struct Layer {
             t.g_ldo = 64 * nxt->sbt.nblk;
             fl += 2.0 * px_out * cout * nxt->cout + 2.0 * V * px_out * nxt->cout;
             by += 4.0 * (px_out * nxt->cout + (double)nxt->cout * cout + (double)V * (V + nxt->cout));
+            t.trash = trash;
+            if (trash && tik::tgw_ok(t)) {
+                // stride 1 + identity residual: the weight-stationary persistent kernel (tgw.hip)
+                const std::string lab = std::string("TW_128.L") + std::to_string(index);
+                static const bool trace = getenv("TIK_TG_TRACE") != nullptr;   // debug: per-phase workgroup timing
+                const int grid = 256;
+                unsigned long long* d = nullptr;
+                if (trace) {
+                    HIP_TRY(hipMalloc(&d, (size_t)1024 * 6 * 8));
+                    HIP_TRY(hipMemset(d, 0, (size_t)1024 * 6 * 8));
+                    t.trace = d;
+                }
+                {
+                    ProfScope p(lab.c_str(), fl, by, st);
+                    p.out(out, (size_t)rout * ldz * 2);
+                    HIP_TRY(tik::launch_tgw(t, st));
+                }
+                if (trace) {
+                    HIP_TRY(hipStreamSynchronize(st));
+                    std::vector<unsigned long long> h((size_t)1024 * 6);
+                    HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipFree(d));
+                    double ph[5] = {0, 0, 0, 0, 0}, tiles = 0;
+                    int nwg = 0;
+                    for (int w = 0; w < 1024; ++w) {
+                        if (!h[6 * w + 5]) continue;
+                        ++nwg; tiles += (double)h[6 * w];
+                        for (int k = 0; k < 5; ++k) ph[k] += (double)h[6 * w + 1 + k];
+                    }
+                    (void)grid;
+                    fprintf(stderr, "TW L%d (%d wg, %.1f tiles/wg): per-tile us loop %.2f epi-image %.2f epi-gcn %.2f epi-mix %.2f | per-wg span %.1f us\n",
+                            index, nwg, tiles / std::max(1, nwg), ph[0] / tiles / 100, ph[1] / tiles / 100, ph[2] / tiles / 100,
+                            ph[3] / tiles / 100, ph[4] / std::max(1, nwg) / 100);
+                }
+                return TIK_OK;
+            }
             const std::string lab = std::string("TG3_128x128.L") + std::to_string(index);
             static const bool trace = getenv("TIK_TG_TRACE") != nullptr;   // debug: per-phase workgroup timing
             const int nwg = (int)((rout + 118) / 119);
@@ -525,6 +561,8 @@ struct tik_model {
     int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
     bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
     bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
+    bool tgw = true;                   // stride-1 fused blocks on the weight-stationary kernel (TIK_TGW=0: TG3)
+    DevHBuf trash;                     // scratch line for the tgw kernel's stores of invalid rows
     Profiler prof;
     bool profiling = false;
 };
@@ -649,13 +687,14 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
     md->prec = default_precision();
-    if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0)))) {
+    if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0))) || (rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
         delete md;
         return rc;
     }
     if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
     if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
+    if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
@@ -805,7 +844,7 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
         const Layer* nxt = (m->fuse_tg && li + 1 < m->layers.size() && L.can_fuse_next(m->layers[li + 1]))
                                ? &m->layers[li + 1] : nullptr;
         if ((rc = L.forward3(cur, ld, N, t, zb[zi], o, m->zeros.p, st, false, raw ? x : nullptr, m->bn_sc.p,
-                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready)))
+                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready, m->tgw ? m->trash.p : nullptr)))
             return rc;
         zready = nxt != nullptr;
         if (nxt) zi ^= 1;

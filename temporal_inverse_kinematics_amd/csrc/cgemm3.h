@@ -54,6 +54,7 @@ struct Cgemm3Args {
     int g_mix_sparse;
     unsigned short* g_out;        // SB z of the next block [M][g_ldo]
     int g_ldo;
+    unsigned short* trash;        // TW_128 (tgw.hip): >= 4 KB scratch line for the stores of invalid rows
     int tune;                     // tuning experiments (0 = production): 1 plain tile order
                                   // instead of the XCD-aware one
     unsigned long long* trace;    // tuning only: per-workgroup {start, loop end, end, wait clk, barrier|loop clk}
@@ -83,6 +84,11 @@ enum TgemmCfg {
     TG_128x128_G7 = 5,   // 7-frame tiles (119 of 128 rows) + the next block's gcn in the epilogue
 };
 hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st);
+
+// weight-stationary persistent T + next gcn (tgw.hip, TW_128): stride 1, identity
+// residual, 128 -> 128 -> 128, V = 17; one workgroup per CU over contiguous tile runs
+bool tgw_ok(const Cgemm3Args& a);
+hipError_t launch_tgw(const Cgemm3Args& a, hipStream_t st);
 
 // stride-1 temporal conv + residual with a frame halo in LDS (tconv.hip):
 // seg[0] kt=3/stride 1/pad 1, optional seg[1] kt=1 (residual conv), V=17,

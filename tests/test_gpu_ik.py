@@ -330,3 +330,22 @@ def test_concurrent_streams_layer0_gcn_bitwise():
             torch.cuda.synchronize()
             for i in range(S):
                 assert torch.equal(outs[i], ref[i])
+
+
+def test_weight_stationary_tgw_bitwise():
+    """The stride-1 fused blocks (L3, L4) on the weight-stationary persistent
+    kernel (tgw.hip, TW_128) give poses bit-identical to the TG3 tiles
+    (TIK_TGW=0) and to the layered G + T path (TIK_FUSE_TG=0): same f16x3
+    products in the same K order, same mix order. Batches: the bench size, a
+    ragged one whose last tile is partial, T=65 windows, and a tiny batch with
+    fewer tiles than CUs."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    tgw = _model_with_env(TIK_SPLIT=0)
+    tg3 = _model_with_env(TIK_TGW=0, TIK_SPLIT=0)
+    plain = _model_with_env(TIK_FUSE_TG=0, TIK_SPLIT=0)
+    for n, T in [(1024, 64), (333, 64), (70, 65), (3, 64)]:
+        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 3)).cuda()
+        with torch.no_grad():
+            y = tgw(x)["poses"]
+            assert torch.equal(y, tg3(x)["poses"]), (n, T)
+            assert torch.equal(y, plain(x)["poses"]), (n, T)

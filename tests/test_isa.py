@@ -1,0 +1,50 @@
+"""Static checks of generated gfx950 code (CPU only: hipcc cross-compiles).
+
+The weight-stationary kernel (csrc/tgw.hip) keeps DMAs of the next tile in
+flight across its epilogue and waits on them with EXACT vmcnt counts, which
+assume every wave issues a fixed number of vector-memory instructions per
+tile: 20 slot + residual LDS-DMA instructions (the slot DMA's third
+instruction is issued by waves 0-3 only), 8 loads of the next gcn's weights,
+and 8 + 8 whole-line stores of out and z'.
+If the compiler merged, split or added any of them (or spilled to scratch),
+those waits would be off: this test compiles the kernel and counts."""
+import os
+import re
+import subprocess
+from collections import Counter
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_tgw_loop_memory_instruction_counts(tmp_path):
+    src = os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", "tgw.hip")
+    out = tmp_path / "tgw.s"
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
+                        "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    lines = out.read_text().split("\n")
+    # the tile loop: the outermost loop whose blocks mention MFMAs; find its header
+    headers = [m.group(1) for l in lines for m in [re.match(r"^\.(LBB\d+_\d+):.*Loop Header: Depth=1", l)] if m]
+    best = None
+    for h in headers:
+        idx = [i for i, l in enumerate(lines) if f"Header={h[1:]} " in l + " " or l.startswith(f".{h}:")]
+        lo, hi = min(idx), max(idx)
+        j = hi + 1
+        while j < len(lines) and not re.match(r"^\.LBB\d+_\d+:", lines[j]):
+            j += 1
+        body = lines[lo:j]
+        if sum("v_mfma" in l for l in body) > (best[0] if best else 0):
+            best = (sum("v_mfma" in l for l in body), body)
+    assert best, "tile loop not found"
+    c = Counter(m.group(1) for l in best[1] for m in [re.match(r"\s+((?:global|buffer|scratch|flat)_\w+)", l)] if m)
+    # 4 slot issues x (2 + 1 conditional) + 8 residual DMAs
+    assert c["buffer_load_dwordx4"] == 20, c
+    # the next gcn's weights: 4 K blocks x (hi, lo)
+    assert c["global_load_dwordx4"] == 8, c
+    # out and z': 8 + 8 whole-line stores per tile
+    assert c["global_store_dwordx4"] == 16, c
+    assert set(c) == {"buffer_load_dwordx4", "global_load_dwordx4", "global_store_dwordx4"}, c

@@ -3,12 +3,14 @@
 // and the third-party smplx.SMPLX.forward it calls (lbs + landmarks).
 //
 // Per call (B bodies):
-//   fk_chain            R_j, J, A_j (B,16,64), pose feature (B,512), first 55 joints
-//   cgemm (T128x128)    v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
-//   cgemm (S128x128)    T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
+//   fk_chain            R_j, J, A_j (B,16,64), pose feature (B,512), first 55 joints (wave per body)
+//   tgemm (TG_128x128)  v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
+//   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
+// (f16x3 on split-block operands; the fp32 precision runs both GEMMs on cgemm.hip)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,6 +18,7 @@
 #include "cgemm.h"
 #include "common.h"
 #include "fk.h"
+#include "cgemm3.h"
 
 using namespace tik_host;
 
@@ -30,13 +33,17 @@ struct tik_fk {
     bool contour = false;
     DevBuf PT;         // [3V][KP]
     DevBuf WT;         // [V][KJ]
-    SplitW sPT, sWT;   // f16 hi/lo planes (PREC_F16X3)
+    SplitW sPT, sWT;   // f16 hi/lo planes (fp32 path's register-staged GEMMs)
+    SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
-    DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra;
-    int nchain = 0;
+    DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra, depth;
+    int nchain = 0, maxdepth = 0;
+    int ldv = 0;       // v_posed row stride (3V rounded up to 4 floats: vector stores)
     // workspace
     DevBuf feat, ablk, vposed, verts_ws;
+    DevHBuf feat_sb, ablk_sb, trash;
+    DevBuf zero_transl;   // (B,3) zeros: the skinning kernel always reads a translation
     DevIBuf dyn_bin;
     int cap = 0;
 };
@@ -112,6 +119,11 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         hdf = to_int(df);
         for (int f : hdf) if (f < 0 || f >= fk->F) return bad("dynamic landmark face index out of range");
     }
+    // depth of each joint in the tree: the chain kernel composes one level at a time
+    std::vector<int> hdepth(NJ, 0);
+    for (int j = 1; j < NJ; ++j) hdepth[j] = hdepth[hpar[j]] + 1;
+    fk->maxdepth = *std::max_element(hdepth.begin(), hdepth.end());
+    fk->ldv = (3 * V + 3) & ~3;
     // neck kinematic chain (smplx: from NECK_IDX=12 up to the root)
     std::vector<int> chain;
     for (int i = 12; i != -1; i = hpar[i]) chain.push_back(i);
@@ -156,7 +168,8 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         (rc = fk->sWT.build(WT, V, 1, KJ, KJ)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
         (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
         (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||
-        (rc = fk->extra.upload(hex))) {
+        (rc = fk->extra.upload(hex)) || (rc = fk->depth.upload(hdepth)) || (rc = fk->bPT.build(PT, 3 * V, 1, KP, KP)) ||
+        (rc = fk->bWT.build(WT, V, 1, KJ, KJ))) {
         delete fk;
         return rc;
     }
@@ -194,7 +207,10 @@ int tik_fk_reserve(tik_fk_t fk, int B) {
     if (B <= fk->cap) return TIK_OK;
     int rc;
     if ((rc = fk->feat.reserve((size_t)B * KP)) || (rc = fk->ablk.reserve((size_t)B * 16 * KJ)) ||
-        (rc = fk->vposed.reserve((size_t)B * 3 * fk->V)) || (rc = fk->dyn_bin.reserve((size_t)B)))
+        (rc = fk->feat_sb.reserve((size_t)B * 2 * KP)) || (rc = fk->ablk_sb.reserve((size_t)B * 16 * 2 * KJ)) ||
+        (rc = fk->vposed.reserve((size_t)B * fk->ldv)) || (rc = fk->dyn_bin.reserve((size_t)B)) ||
+        (rc = fk->zero_transl.upload(std::vector<float>((size_t)B * 3, 0.f))) ||
+        (!fk->trash.p && (rc = fk->trash.upload(std::vector<unsigned short>(4096, 0)))))
         return rc;
     fk->cap = B;
     return TIK_OK;
@@ -211,27 +227,46 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         if ((rc = fk->verts_ws.reserve((size_t)B * 3 * fk->V))) return rc;
         vout = fk->verts_ws.p;
     }
+    const bool f16x3 = fk->prec == tik::PREC_F16X3;
     tik::FkChainArgs c{};
     c.B = B; c.nb = fk->nb; c.ne = fk->ne; c.kp = KP; c.kj = KJ; c.njoints = fk->njoints; c.nchain = fk->nchain;
     c.pose = full_pose; c.betas = betas; c.expr = expression; c.transl = transl; c.pose_mean = fk->pose_mean.p;
     c.parents = fk->parents.p; c.chain = fk->chain.p; c.jt = fk->jt.p; c.jd = fk->jd.p;
-    c.feat = fk->feat.p; c.ablk = fk->ablk.p; c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
+    c.feat = f16x3 ? nullptr : fk->feat.p; c.ablk = f16x3 ? nullptr : fk->ablk.p;
+    c.feat_sb = f16x3 ? fk->feat_sb.p : nullptr; c.ablk_sb = f16x3 ? fk->ablk_sb.p : nullptr;
+    c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
+    c.depth = fk->depth.p; c.maxdepth = fk->maxdepth;
     HIP_TRY(tik::launch_fk_chain(c, st));
 
     const int V3 = 3 * fk->V;
-    tik::CgemmArgs g{};   // v_posed = feat . P
-    g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
-    g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
-    g.seg[0].whi = fk->sPT.hi.p; g.seg[0].wlo = fk->sPT.lo.p; g.seg[0].cin8 = fk->sPT.cin8; g.seg[0].ldw8 = fk->sPT.ldw8;
-    g.nseg = 1; g.out = fk->vposed.p; g.ldo = V3; g.act = tik::ACT_NONE;
-    HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
+    if (f16x3) {
+        // v_posed = feat . P on split-block operands (tgemm.hip: LDS-DMA rings, f16x3 MFMA)
+        tik::Cgemm3Args g{};
+        g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
+        g.seg[0] = tik::Seg3{fk->feat_sb.p, KP / 32, 2 * KP, 1, 1, 0, B, fk->bPT.w.p, fk->bPT.ldw};
+        g.nseg = 1; g.out_f = fk->vposed.p; g.ldf = fk->ldv; g.act = tik::ACT_NONE;
+        HIP_TRY(tik::launch_tgemm(g, tik::TG_128x128, st));
+        // skinning + vertex transform (fk.hip)
+        tik::FkSkinArgs s{};
+        s.B = B; s.V = fk->V; s.kj = KJ; s.ablk_sb = fk->ablk_sb.p; s.w_sb = fk->bWT.w.p;
+        s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
+        s.trash = fk->trash.p;
+        HIP_TRY(tik::launch_fk_skin(s, st));
+    } else {
+        tik::CgemmArgs g{};   // v_posed = feat . P
+        g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
+        g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
+        g.seg[0].whi = fk->sPT.hi.p; g.seg[0].wlo = fk->sPT.lo.p; g.seg[0].cin8 = fk->sPT.cin8; g.seg[0].ldw8 = fk->sPT.ldw8;
+        g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
+        HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
 
-    tik::CgemmArgs s{};   // skinning + vertex transform
-    s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
-    s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
-    s.seg[0].whi = fk->sWT.hi.p; s.seg[0].wlo = fk->sWT.lo.p; s.seg[0].cin8 = fk->sWT.cin8; s.seg[0].ldw8 = fk->sWT.ldw8;
-    s.nseg = 1; s.resid = fk->vposed.p; s.ldr = V3; s.out = vout; s.ldo = V3; s.bias = transl;
-    HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
+        tik::CgemmArgs s{};   // skinning + vertex transform
+        s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
+        s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
+        s.seg[0].whi = fk->sWT.hi.p; s.seg[0].wlo = fk->sWT.lo.p; s.seg[0].cin8 = fk->sWT.cin8; s.seg[0].ldw8 = fk->sWT.ldw8;
+        s.nseg = 1; s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl;
+        HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
+    }
 
     tik::FkLmkArgs l{};
     l.B = B; l.V = fk->V; l.njoints = fk->njoints; l.nextra = fk->nextra; l.nlmk = fk->nlmk; l.ndyn = fk->ndyn;

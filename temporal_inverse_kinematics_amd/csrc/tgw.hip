@@ -55,29 +55,6 @@ static_assert(RT * LDY * 4 <= 4 * EB, "Y fits the E region");
 static_assert(SMEM <= 160 * 1024, "LDS");
 }  // namespace tw
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 63]
-__device__ __forceinline__ void wait_vm_dyn(int n) {
-    switch (n) {
-#define TIK_VMW(k) \
-    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-        TIK_VMW(0) TIK_VMW(1) TIK_VMW(2) TIK_VMW(3) TIK_VMW(4) TIK_VMW(5) TIK_VMW(6) TIK_VMW(7)
-        TIK_VMW(8) TIK_VMW(9) TIK_VMW(10) TIK_VMW(11) TIK_VMW(12) TIK_VMW(13) TIK_VMW(14) TIK_VMW(15)
-        TIK_VMW(16) TIK_VMW(17) TIK_VMW(18) TIK_VMW(19) TIK_VMW(20) TIK_VMW(21) TIK_VMW(22) TIK_VMW(23)
-        TIK_VMW(24) TIK_VMW(25) TIK_VMW(26) TIK_VMW(27) TIK_VMW(28) TIK_VMW(29) TIK_VMW(30) TIK_VMW(31)
-        TIK_VMW(32) TIK_VMW(33) TIK_VMW(34) TIK_VMW(35) TIK_VMW(36) TIK_VMW(37) TIK_VMW(38) TIK_VMW(39)
-        TIK_VMW(40) TIK_VMW(41) TIK_VMW(42) TIK_VMW(43) TIK_VMW(44) TIK_VMW(45) TIK_VMW(46) TIK_VMW(47)
-        TIK_VMW(48) TIK_VMW(49) TIK_VMW(50) TIK_VMW(51) TIK_VMW(52) TIK_VMW(53) TIK_VMW(54) TIK_VMW(55)
-        TIK_VMW(56) TIK_VMW(57) TIK_VMW(58) TIK_VMW(59) TIK_VMW(60) TIK_VMW(61) TIK_VMW(62) TIK_VMW(63)
-#undef TIK_VMW
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-}
-
 __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
     using namespace tw;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];   // the only LDS object

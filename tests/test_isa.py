@@ -48,3 +48,32 @@ def test_tgw_loop_memory_instruction_counts(tmp_path):
     # out and z': 8 + 8 whole-line stores per tile
     assert c["global_store_dwordx4"] == 16, c
     assert set(c) == {"buffer_load_dwordx4", "global_load_dwordx4", "global_store_dwordx4"}, c
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_fk_skin_loop_memory_instruction_counts(tmp_path):
+    """The persistent skinning kernel (csrc/fk.hip) waits on its double-buffered
+    A tiles with exact vmcnt counts: per body tile and wave 4 LDS-DMA
+    instructions, 8 v_posed loads (one dwordx3 per vertex), 4 translation
+    loads and 8 vertex stores (fks::NDA, NLD, NST); the loop holds two steps."""
+    src = os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", "fk.hip")
+    out = tmp_path / "fk.s"
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
+                        "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    lines = out.read_text().split("\n")
+    st = [i for i, l in enumerate(lines) if l.startswith("_ZN3tik14fk_skin_kernel")][0]
+    en = [i for i, l in enumerate(lines) if i > st and "s_endpgm" in l][0]
+    body = lines[st:en]
+    hdr = [re.match(r"^\.(LBB\d+_\d+):", l).group(1) for l in body if "Loop Header: Depth=1" in l]
+    assert len(hdr) == 1, hdr
+    h = hdr[0]
+    idx = [i for i, l in enumerate(body) if f"Header={h[1:]} " in l + " " or l.startswith(f".{h}:")]
+    lo, hi = min(idx), max(idx)
+    j = hi + 1
+    while j < len(body) and not re.match(r"^\.LBB\d+_\d+:", body[j]):
+        j += 1
+    c = Counter(m.group(1) for l in body[lo:j] for m in [re.match(r"\s+((?:global|buffer|scratch|flat)_\w+)", l)] if m)
+    # the loop body holds two tile steps (unrolled by two for the static prefetch buffers)
+    assert c == Counter({"buffer_load_dwordx4": 8, "global_load_dwordx3": 16, "global_load_dword": 8,
+                         "global_store_dword": 16}), c

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int M = a.M, nfo = a.M / 17, T = a.tout;
     // debug (a.trace): per-workgroup phase sums over its tiles, in s_memrealtime ticks
-    unsigned long long tr_loop = 0, tr_epi1 = 0, tr_epi2 = 0, tr_epi3 = 0;
+    unsigned long long tr_loop = 0, tr_epi1 = 0, tr_epi2 = 0, tr_epi3 = 0, tr_wait = 0, tr_bar = 0;
     const unsigned long long ts_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // ---- this workgroup's contiguous run of tiles (runs ordered per XCD)
@@ -251,7 +251,9 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         wait_vm_dyn(0);
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) asm volatile("" : "+v"(wgh[kb]), "+v"(wgl[kb]));
+        const unsigned long long tsw = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         lds_barrier();   // ... for every wave; and every wave is done with the four slots
+        const unsigned long long tsb = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         // (2) out = ReLU(C + bias + x) -> the split image of out, IN PLACE of the residual
         // image: each (pixel, 4-channel) piece is read and rewritten by the same lane
         // (all reads first: one LDS round trip, not one per fragment)
@@ -403,14 +405,16 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         if (a.trace) {
             const unsigned long long ts4 = __builtin_amdgcn_s_memrealtime();
             tr_loop += ts1 - ts0; tr_epi1 += ts2 - ts1; tr_epi2 += ts3 - ts2; tr_epi3 += ts4 - ts3;
+            tr_wait += tsw - ts1; tr_bar += tsb - tsw;
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (a.trace && tid == 0) {   // {tiles, loop, epilogue to image, to Y, mix + z', span}
-        unsigned long long* tr = a.trace + 6 * (size_t)blockIdx.x;
+    if (a.trace && tid == 0) {   // {tiles, loop, epilogue to image, to Y, mix + z', span, E1 wait, E1 barrier}
+        unsigned long long* tr = a.trace + 8 * (size_t)blockIdx.x;
         tr[0] = (unsigned long long)(t_end - t_begin);
         tr[1] = tr_loop; tr[2] = tr_epi1; tr[3] = tr_epi2; tr[4] = tr_epi3;
         tr[5] = __builtin_amdgcn_s_memrealtime() - ts_start;
+        tr[6] = tr_wait; tr[7] = tr_bar;
     }
 }
 

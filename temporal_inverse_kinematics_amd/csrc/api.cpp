@@ -353,36 +353,6 @@ struct Layer {
                         2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * TK * cout * cout,
                         4.0 * (px_in * cin + px_out * cout + (double)cout * cin + (double)TK * cout * cout), st);
             static const bool trace = getenv("TIK_STB_TRACE") != nullptr;
-            static const bool stb2 = !(getenv("TIK_STB2") && getenv("TIK_STB2")[0] == '0');
-            if (stb2 && trash && cin == 64 && cout == 64) {
-                // persistent, weight-stationary variant (stb2.hip)
-                b.trash = trash;
-                unsigned long long* d = nullptr;
-                if (trace) {
-                    HIP_TRY(hipMalloc(&d, (size_t)1024 * 6 * 8));
-                    HIP_TRY(hipMemset(d, 0, (size_t)1024 * 6 * 8));
-                    b.trace = d;
-                }
-                p.out(out, (size_t)rout * ldz * 2);
-                HIP_TRY(tik::launch_stb2(b, st));
-                if (trace) {
-                    HIP_TRY(hipStreamSynchronize(st));
-                    std::vector<unsigned long long> h((size_t)1024 * 6);
-                    HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                    HIP_TRY(hipFree(d));
-                    double ph[5] = {0, 0, 0, 0, 0}, tiles = 0;
-                    int nwg = 0;
-                    for (int w = 0; w < 1024; ++w) {
-                        if (!h[6 * w + 5]) continue;
-                        ++nwg; tiles += (double)h[6 * w];
-                        for (int k = 0; k < 5; ++k) ph[k] += (double)h[6 * w + 1 + k];
-                    }
-                    fprintf(stderr, "B3P L%d (%d wg, %.1f tiles/wg): per-tile us wait+G %.2f resid+mix %.2f T %.2f epi %.2f | span %.1f us\n",
-                            index, nwg, tiles / std::max(1, nwg), ph[0] / tiles / 100, ph[1] / tiles / 100, ph[2] / tiles / 100,
-                            ph[3] / tiles / 100, ph[4] / std::max(1, nwg) / 100);
-                }
-                return TIK_OK;
-            }
             if (!trace) {
                 p.out(out, (size_t)rout * ldz * 2);
                 HIP_TRY(tik::launch_stblock(b, cin, cout, st));

@@ -131,14 +131,12 @@ struct StbArgs {
     const float* wg0;           // fp32 gcn weights (tcn.0 BN folded) [Cout][ldwg0]
     int ldwg0;
     const float* rw;            // fp32 residual conv (BN folded) [Cout][c0]
-    unsigned short* trash;      // launch_stb2: >= 4 KB scratch line for the stores of invalid rows
 };
 bool stblock_ok(int cin, int cout);
 hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st);
 // the whole FIRST block from the raw keypoints (Cout = 64, stride 1, residual conv)
 hipError_t launch_stblock0(const StbArgs& a, int cout, hipStream_t st);
-// persistent, weight-stationary 64 -> 64 identity block (stb2.hip, B3_64P)
-hipError_t launch_stb2(const StbArgs& a, hipStream_t st);
+
 
 hipError_t launch_merge(const unsigned short* sb, long long rows, int C, int ld, float* y, hipStream_t st);
 // data_bn on load, straight to one SB block per pixel (C <= 32 channels, rest zero) (st_gcn_aaai18.py:119-125)

@@ -350,15 +350,3 @@ def test_weight_stationary_tgw_bitwise():
             assert torch.equal(y, tg3(x)["poses"]), (n, T)
             assert torch.equal(y, plain(x)["poses"]), (n, T)
 
-
-def test_persistent_whole_block_bitwise():
-    """Layer 1 (64 -> 64 identity block) on the persistent weight-stationary
-    whole-block kernel (stb2.hip, B3_64P) gives poses bit-identical to
-    stblock.hip's B3_64 (TIK_STB2=0): same products, K orders and mix order."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    new = _model_with_env(TIK_SPLIT=0)
-    old = _model_with_env(TIK_STB2=0, TIK_SPLIT=0)
-    for n, T in [(1024, 64), (333, 64), (70, 65), (3, 64), (1, 9)]:
-        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 5)).cuda()
-        with torch.no_grad():
-            assert torch.equal(new(x)["poses"], old(x)["poses"]), (n, T)

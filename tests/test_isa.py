@@ -78,33 +78,3 @@ def test_fk_skin_loop_memory_instruction_counts(tmp_path):
     assert c == Counter({"buffer_load_dwordx4": 8, "global_load_dwordx3": 16, "global_load_dword": 8,
                          "global_store_dword": 16}), c
 
-
-def _loop_counts(src_name, kernel_prefix=None):
-    import tempfile
-    src = os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", src_name)
-    with tempfile.TemporaryDirectory() as td:
-        out = os.path.join(td, "k.s")
-        r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
-                            "--cuda-device-only", "-S", src, "-o", out], capture_output=True, text=True)
-        assert r.returncode == 0, r.stderr
-        lines = open(out).read().split("\n")
-    best = None
-    for h in [m.group(1) for l in lines for m in [re.match(r"^\.(LBB\d+_\d+):.*Loop Header: Depth=1", l)] if m]:
-        idx = [i for i, l in enumerate(lines) if f"Header={h[1:]} " in l + " " or l.startswith(f".{h}:")]
-        lo, hi = min(idx), max(idx)
-        j = hi + 1
-        while j < len(lines) and not re.match(r"^\.LBB\d+_\d+:", lines[j]):
-            j += 1
-        n = sum("v_mfma" in l for l in lines[lo:j])
-        if best is None or n > best[0]:
-            best = (n, lines[lo:j])
-    return Counter(m.group(1) for l in best[1] for m in [re.match(r"\s+((?:global|buffer|scratch|flat)_\w+)", l)] if m)
-
-
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_stb2_loop_memory_instruction_counts():
-    """The persistent whole-block kernel (csrc/stb2.hip) waits with exact vmcnt
-    counts: per tile and wave 16 residual loads, 9 x-image LDS-DMA
-    instructions and 8 whole-line stores (s2::NRL, NX, NST), nothing else."""
-    c = _loop_counts("stb2.hip")
-    assert c == Counter({"global_load_dwordx2": 16, "buffer_load_dwordx4": 9, "global_store_dwordx4": 8}), c

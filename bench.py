@@ -36,6 +36,7 @@ KERNEL_SYMBOLS = {
     "T3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 0>",
     "T3_128x64": "tik::tgemm_kernel<128, 64, 4, 2, 3, 0>",
     "TG3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 7>",
+    "TW_128": "tik::tgw_kernel",
     "TH_128x128": "tik::tconv_halo_kernel<128, 2, 4>",
     "TH_128x64": "tik::tconv_halo_kernel<64, 4, 2>",
     "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",

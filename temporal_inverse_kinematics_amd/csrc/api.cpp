@@ -545,15 +545,17 @@ struct tik_model {
     // ws[1] + a private stream: large f16x3 batches run as two halves on two
     // streams, so one half's launches fill the other's tails and epilogues.
     // Online-IK streams own their workspaces (stream.cpp).
-    Workspace ws[2];
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    static constexpr int MAXSPLIT = 4;
+    Workspace ws[MAXSPLIT];
+    hipStream_t aux[MAXSPLIT - 1] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT - 1] = {};
     bool split = true;                 // TIK_SPLIT=0: one stream
+    int nsplit = 2;                    // parts of a split batch (TIK_SPLIT_N, 2..4)
     std::atomic<int> refs{1};          // the handle + every live online-IK stream
     ~tik_model() {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (aux) (void)hipStreamDestroy(aux);
+        for (auto e : ev_join) if (e) (void)hipEventDestroy(e);
+        for (auto a : aux) if (a) (void)hipStreamDestroy(a);
     }
     DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
     long long dma_min_frames = 1;      // f16x3: N*T at or above -> split-activation DMA path (TIK_GEMM_PATH)
@@ -696,6 +698,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
     if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
+    if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
         if (!strcmp(e, "dma")) md->dma_min_frames = 1;
@@ -762,14 +765,16 @@ struct WsPtrs {
     float *xb, *z, *z2, *a0, *a1, *hid, *part;
 };
 static WsPtrs ptrs_of(const Workspace& w) { return WsPtrs{w.xb.p, w.z.p, w.z2.p, w.a0.p, w.a1.p, w.hid.p, w.part.p}; }
-// the second workspace set (split halves) and the aux stream
-static int reserve_b(tik_model* m, int N, int T) {
+// the workspaces and aux streams of the parts 1 .. np-1 of a split batch
+static int reserve_parts(tik_model* m, int np, int N, int T) {
     int rc;
-    if ((rc = model_reserve_ws(m, m->ws[1], N, T))) return rc;
-    if (!m->aux) {
-        HIP_TRY(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+    if (!m->ev_fork) HIP_TRY(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+    for (int k = 1; k < np; ++k) {
+        if ((rc = model_reserve_ws(m, m->ws[k], N, T))) return rc;
+        if (!m->aux[k - 1]) {
+            HIP_TRY(hipStreamCreateWithFlags(&m->aux[k - 1], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&m->ev_join[k - 1], hipEventDisableTiming));
+        }
     }
     return TIK_OK;
 }
@@ -956,7 +961,8 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
         // two halves on two streams when the batch is large (not while profiling:
         // per-launch events would time overlapping kernels)
         const bool split = allow_split && m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
-        if (split && (rc = reserve_b(m, (std::min(N, chunk) + 1) / 2, T))) return rc;
+        const int np = split ? std::min(m->nsplit, std::min(N, chunk)) : 1;
+        if (split && (rc = reserve_parts(m, np, (std::min(N, chunk) + np - 1) / np, T))) return rc;
         auto half = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w) -> int {
             const half_t* fs;
             int ld, r;
@@ -974,16 +980,20 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
             const float* xs = x + (size_t)n0 * T * m->V * m->C0;
             const int To = tik_model_out_frames(m, T);
             float* ps = poses + (size_t)n0 * To * m->pose_dim;
-            if (split && n >= 2 && (long long)n * T >= 32768) {
-                const int na = n / 2, nb = n - na;
+            if (split && n >= np && (long long)n * T >= 32768) {
+                // np parts on np streams (the caller's + handle-owned ones), fork/join by events
                 HIP_TRY(hipEventRecord(m->ev_fork, st));
-                HIP_TRY(hipStreamWaitEvent(m->aux, m->ev_fork, 0));
-                if ((rc = half(xs, na, ps, st, ptrs_of(ws)))) return rc;
-                if ((rc = half(xs + (size_t)na * T * m->V * m->C0, nb, ps + (size_t)na * To * m->pose_dim, m->aux,
-                               ptrs_of(m->ws[1]))))
-                    return rc;
-                HIP_TRY(hipEventRecord(m->ev_join, m->aux));
-                HIP_TRY(hipStreamWaitEvent(st, m->ev_join, 0));
+                for (int k = 1; k < np; ++k) HIP_TRY(hipStreamWaitEvent(m->aux[k - 1], m->ev_fork, 0));
+                for (int k = 0; k < np; ++k) {
+                    const int a0 = (int)((long long)n * k / np), a1 = (int)((long long)n * (k + 1) / np);
+                    if ((rc = half(xs + (size_t)a0 * T * m->V * m->C0, a1 - a0, ps + (size_t)a0 * To * m->pose_dim,
+                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]))))
+                        return rc;
+                }
+                for (int k = 1; k < np; ++k) {
+                    HIP_TRY(hipEventRecord(m->ev_join[k - 1], m->aux[k - 1]));
+                    HIP_TRY(hipStreamWaitEvent(st, m->ev_join[k - 1], 0));
+                }
             } else if ((rc = half(xs, n, ps, st, ptrs_of(ws)))) {
                 return rc;
             }

@@ -38,9 +38,11 @@ def main():
     out = {"metric": "online IK per-frame latency (p50)", "value": round(float(np.percentile(lat_us, 50)), 2),
            "unit": "us", "higher_is_better": False, "p99_us": round(float(np.percentile(lat_us, 99)), 2),
            "mean_us": round(float(lat_us.mean()), 2), "frames_per_s": round(a.frames / lat.sum(), 1),
-           "n_gpus": 1, "dtype": a.precision,
+           "n_gpus": 1, "dtype": "fp32" if s.path == "dataflow" else a.precision, "step": s.path,
            "config": {"workload": f"stride-1 sliding window, win_size={a.win} (T={2 * (a.win // 2) + 1}), B=1, "
-                                  f"{'hipGraph replay' if not a.no_graph else 'eager launches'} per frame",
+                                  f"{'hipGraph replay' if not a.no_graph else 'eager launches'} per frame"
+                                  + (" (one dataflow kernel, only the frames pose row 0 depends on)"
+                                     if s.path == "dataflow" else " (layered forward on the whole window)"),
                       "frames": a.frames, "warmup": a.warmup}}
     print(json.dumps(out))
 

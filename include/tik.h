@@ -153,6 +153,17 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
 int tik_stream_destroy(tik_stream_t s);
 int tik_stream_reset(tik_stream_t s);
 int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host);
+/* Which step the stream runs: 1 = the single dataflow kernel (online.hip:
+ * only the frames pose row 0 depends on, fp32, frame read from and pose
+ * written to pinned host memory by the kernel; TIK_ONLINE=0 disables it),
+ * 0 = the layered IK forward on the whole window (models it cannot run). */
+int tik_stream_path(tik_stream_t s);
+/* Debug (TIK_ONLINE_TRACE=1 at create): the last step's per-task timestamps
+ * {ticket taken, inputs ready, staged, computed, reduced, stores complete,
+ * done, workgroup} (s_memrealtime ticks, 100 MHz; staged .. reduced: gcn and
+ * temporal-conv tasks only)
+ * in task order; returns the task count. */
+int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap);
 
 /* ------------------------------------------------------------------------
  * SMPL-X forward kinematics + linear blend skinning (the FK check).

@@ -25,6 +25,7 @@
 #include "cgemm.h"
 #include "cgemm3.h"
 #include "misc.h"
+#include "online.h"
 #include "common.h"
 
 namespace tik_host {
@@ -751,6 +752,27 @@ int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
 void model_retain(tik_model* m) { m->refs.fetch_add(1); }
 void model_release(tik_model* m) {
     if (m->refs.fetch_sub(1) == 1) delete m;
+}
+
+int model_online_fill(tik_model* m, tik::OnlineArgs& a) {
+    static_assert((int)tik::ONR_ZERO == RES_ZERO && (int)tik::ONR_IDEN == RES_IDEN && (int)tik::ONR_CONV == RES_CONV, "");
+    const int nl = (int)m->layers.size();
+    if (m->V != 17 || m->C0 != 3 || nl > tik::ONL_MAXL) return fail(TIK_E_INVALID, "online kernel: V=17, 3 input channels, <= %d layers", tik::ONL_MAXL);
+    a.nl = nl;
+    for (int l = 0; l < nl; ++l) {
+        const Layer& L = m->layers[l];
+        if (L.cout % 16 || L.cout > tik::ONL_MAXC || L.cinp > tik::ONL_MAXC || (l > 0 && L.cinp != L.cin))
+            return fail(TIK_E_INVALID, "online kernel: layer %d channels %d -> %d", l, L.cin, L.cout);
+        tik::OnlineLayer& o = a.L[l];
+        o.cin = L.cin; o.cinp = L.cinp; o.cout = L.cout; o.stride = L.stride; o.res = L.res;
+        o.wg = L.wg.p; o.bias2 = L.bias2.p; o.amix = L.amix.p; o.wt = L.wt.p; o.wr = L.wr.p; o.biasT = L.biasT.p;
+    }
+    if (m->feat % 4 || m->feat > tik::ONL_MAXHC * 256 || m->hidden % 16 || m->hidden > tik::ONL_MAXHC * 256)
+        return fail(TIK_E_INVALID, "online kernel: head %d -> %d", m->feat, m->hidden);
+    a.w0 = m->w0.p; a.b0 = m->b0.p; a.w3 = m->w3.p; a.b3 = m->b3.p;
+    a.feat = m->feat; a.hidden = m->hidden; a.pose_dim = m->pose_dim;
+    a.bn_sc = m->bn_sc.p; a.bn_sh = m->bn_sh.p;
+    return TIK_OK;
 }
 }  // namespace tik_host
 

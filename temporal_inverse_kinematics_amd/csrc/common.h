@@ -198,6 +198,7 @@ struct Workspace {
 }  // namespace tik_host
 
 struct tik_model;
+namespace tik { struct OnlineArgs; }
 namespace tik_host {
 // internal entry points shared by api.cpp and stream.cpp
 int model_reserve_ws(tik_model* m, Workspace& w, int N, int T);
@@ -206,6 +207,9 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
                      bool split);
 void model_retain(tik_model* m);    // a stream keeps its model alive
 void model_release(tik_model* m);   // deletes the model at the last reference
+// the fp32 weights and shapes of the online-IK dataflow kernel (online.h);
+// TIK_E_INVALID when the model is outside what that kernel supports
+int model_online_fill(tik_model* m, tik::OnlineArgs& a);
 
 
 }  // namespace tik_host

@@ -1,0 +1,72 @@
+// online.h — the online-IK step as ONE dataflow kernel (online.hip).
+//
+// The stream returns pose row 0 of the window's output (stream.cpp), and with
+// 3x1 temporal convs row 0 only sees the first frames of every layer: output
+// frame t of a stride-s layer reads input frames s*t-1 .. s*t+1. Walking that
+// back from the head gives each layer's needed frame count (n_out, n_in; 1,
+// 2, 4, 8, 9, 10, 20, 21, 22 input frames for the IK net at any window of at
+// least 22 frames). The step computes exactly those frames, in fp32 VALU
+// arithmetic, as a list of small tasks in topological order:
+//   INPUT: ring append of the new frame (read from pinned host memory),
+//          window gather (left-edge clamp), root-relative, data_bn
+//   G_L(f, 16 channels): gcn 1x1 conv + 17x17 graph mix + bias + ReLU
+//   T_L(t, 16 channels): 3x1 temporal conv + residual + bias + ReLU
+//   H0(16 hidden units), H1(16 pose values, written straight to pinned host memory)
+// Workgroups take task tickets in order and wait only on per-frame completion
+// counters of the frames a task reads (no grid-wide barrier), so the layers
+// pipeline frame by frame; a task's weights are loaded before it waits.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace tik {
+
+constexpr int ONL_MAXL = 12;        // layers
+constexpr int ONL_MAXC = 256;       // channels per layer
+constexpr int ONL_MAXHC = 20;       // head K chunks of 4 per lane: K <= 20 * 4 * 64 = 5120
+enum { ONP_INPUT = 0, ONP_G = 1, ONP_T = 2, ONP_H0 = 3, ONP_H1 = 4 };
+enum { ONR_ZERO = 0, ONR_IDEN = 1, ONR_CONV = 2 };
+
+struct OnlineLayer {
+    int cin, cinp, cout, stride, res;
+    int tin;           // the layer's real input frame count (zero padding past it)
+    int n_in, n_out;   // frames computed: z (gcn) / out (temporal conv)
+    const float *wg, *bias2, *amix, *wt, *wr, *biasT;   // the fp32 folded weights of api.cpp's Layer
+    const float* x;    // input rows [n_in][17][cinp]
+    float *z, *out;    // [n_in][17][cout], [n_out][17][cout]
+};
+
+struct OnlinePhase {
+    int kind, layer, nframes, ngroups, task0, cbase;   // cbase: first completion counter (one per frame)
+};
+
+struct OnlineArgs {
+    int nl, nph, ntasks;
+    OnlineLayer L[ONL_MAXL];
+    OnlinePhase ph[2 * ONL_MAXL + 3];
+    // input: ring of W frames (V*3 floats), count of frames pushed so far
+    float* ring;
+    int W, h, ra, rb, relative;
+    int* count;
+    const float* frame;   // the pushed frame (pinned host memory)
+    const float *bn_sc, *bn_sh;
+    float* x0;            // [n_in0][17][4]
+    // head
+    const float *w0, *b0, *w3, *b3;
+    int feat, hidden, pose_dim;
+    float* hid;
+    float* pose;          // device copy of the pose row
+    float* pose_host;     // pinned host copy
+    // scheduling state: zero at launch, left zero by the last workgroup out
+    int* ticket;
+    int* done;
+    int* cnt;
+    int ncnt;
+    int* err;             // sticky: a dependency wait timed out
+    unsigned long long* trace;   // debug (TIK_ONLINE_TRACE=1): per task {grab, inputs ready, done, workgroup}
+    float* act;           // the one buffer every inter-task activation lives in (x0, z, out, hid)
+    unsigned act_bytes;
+};
+
+hipError_t launch_online(const OnlineArgs* dev_args, int grid, hipStream_t st);
+
+}  // namespace tik

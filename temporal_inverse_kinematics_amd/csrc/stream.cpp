@@ -6,14 +6,20 @@
 // (frames k-2h..k, left edge clamped like sample_window's edge padding) and
 // returns pose row 0 of the model output, i.e. exactly run_inference's frame c.
 // Flushing the last h frames = pushing the last frame h more times (right edge
-// padding). The whole step — ring append, window gather, the ~20 kernels of the
-// IK forward, the pose copy — is one hipGraph replay on a private stream.
+// padding). Default step: ONE dataflow kernel (online.hip) that reads the
+// frame from pinned host memory, appends it to the ring, computes only the
+// frames pose row 0 depends on, and writes the pose to pinned host memory.
+// Fallback step (TIK_ONLINE=0, or a model that kernel does not cover): ring
+// append, window gather, the layered IK forward on the whole window, the pose
+// copy. Either is one hipGraph replay on a private stream when use_graph.
 #include <hip/hip_runtime.h>
 
 #include "../../include/tik.h"
 #include "common.h"
 #include "misc.h"
+#include "online.h"
 
+#include <algorithm>
 #include <cstring>
 
 using namespace tik_host;
@@ -28,8 +34,16 @@ struct tik_stream {
     DevBuf ring, window, poses, frame_in, pose_out;
     DevIBuf count;
     float* host_frame = nullptr;   // pinned
-    float* host_pose = nullptr;    // pinned
+    float* host_pose = nullptr;    // pinned; [pose_dim] = the online kernel's error flag
     long long pushed = 0;
+    // the dataflow step (online.hip)
+    bool online = false;
+    int onl_grid = 0;
+    DevBuf onl_act;                       // every activation of the step
+    DevIBuf onl_cnt;                      // completion counters, ticket, done, err
+    DevArray<tik::OnlineArgs> onl_args;   // the kernel's argument block
+    DevArray<unsigned long long> onl_trace;   // TIK_ONLINE_TRACE=1
+    int onl_ntasks = 0;
     ~tik_stream() {
         if (st) (void)hipStreamSynchronize(st);
         if (exec) (void)hipGraphExecDestroy(exec);
@@ -41,7 +55,91 @@ struct tik_stream {
     }
 };
 
+static int cu_count() {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return 256;
+    return c;
+}
+
+// frames each layer must compute for pose row 0, buffers, task list (online.h)
+static int setup_online(tik_stream* s) {
+    tik::OnlineArgs a{};
+    int rc = model_online_fill(s->model, a);
+    if (rc) return rc;
+    const int nl = a.nl;
+    int t = s->W;
+    for (int l = 0; l < nl; ++l) {
+        a.L[l].tin = t;
+        t = (t - 1) / a.L[l].stride + 1;
+    }
+    int need = 1;   // the last layer's output frames: row 0
+    for (int l = nl - 1; l >= 0; --l) {
+        tik::OnlineLayer& L = a.L[l];
+        L.n_out = need;
+        L.n_in = std::min(L.tin, L.stride * (need - 1) + 2);
+        need = L.n_in;
+    }
+    size_t tot = (size_t)a.L[0].n_in * 17 * 4 + a.hidden + ((a.pose_dim + 3) & ~3);
+    for (int l = 0; l < nl; ++l) tot += (size_t)(a.L[l].n_in + a.L[l].n_out) * 17 * a.L[l].cout;
+    if ((rc = s->onl_act.reserve(tot))) return rc;
+    float* q = s->onl_act.p;
+    a.x0 = q; q += (size_t)a.L[0].n_in * 17 * 4;
+    for (int l = 0; l < nl; ++l) {
+        tik::OnlineLayer& L = a.L[l];
+        L.x = l == 0 ? a.x0 : a.L[l - 1].out;
+        L.z = q; q += (size_t)L.n_in * 17 * L.cout;
+        L.out = q; q += (size_t)L.n_out * 17 * L.cout;
+    }
+    a.hid = q; q += a.hidden;
+    a.pose = q;
+    a.act = s->onl_act.p;
+    a.act_bytes = (unsigned)(tot * sizeof(float));
+    int np = 0, task = 0, cb = 0;
+    auto add = [&](int kind, int layer, int nf, int ng) {
+        a.ph[np++] = tik::OnlinePhase{kind, layer, nf, ng, task, cb};
+        task += nf * ng;
+        cb += nf;
+    };
+    add(tik::ONP_INPUT, 0, 1, 1);
+    for (int l = 0; l < nl; ++l) {
+        add(tik::ONP_G, l, a.L[l].n_in, a.L[l].cout / 16);
+        add(tik::ONP_T, l, a.L[l].n_out, a.L[l].cout / 16);
+    }
+    add(tik::ONP_H0, nl - 1, 1, a.hidden / 16);
+    add(tik::ONP_H1, nl - 1, 1, (a.pose_dim + 15) / 16);
+    a.nph = np;
+    a.ntasks = task;
+    if ((rc = s->onl_cnt.reserve(cb + 3))) return rc;
+    HIP_TRY(hipMemset(s->onl_cnt.p, 0, sizeof(int) * (cb + 3)));
+    a.cnt = s->onl_cnt.p; a.ncnt = cb;
+    a.ticket = a.cnt + cb; a.done = a.cnt + cb + 1; a.err = a.cnt + cb + 2;
+    a.ring = s->ring.p; a.W = s->W; a.h = s->h; a.ra = 11; a.rb = 12; a.relative = 1;
+    a.count = s->count.p;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, s->host_frame, 0));
+    a.frame = static_cast<const float*>(dp);
+    HIP_TRY(hipHostGetDevicePointer(&dp, s->host_pose, 0));
+    a.pose_host = static_cast<float*>(dp);
+    a.trace = nullptr;
+    if (const char* e = getenv("TIK_ONLINE_TRACE"); e && e[0] == '1') {
+        if ((rc = s->onl_trace.reserve((size_t)8 * task))) return rc;
+        a.trace = s->onl_trace.p;
+    }
+    s->onl_ntasks = task;
+    if ((rc = s->onl_args.upload(std::vector<tik::OnlineArgs>{a}))) return rc;
+    // half the CUs: more workgroups only add pollers (measured p50 143 us at 128, 151 us at 256)
+    int grid = std::max(1, cu_count() / 2);
+    if (const char* e = getenv("TIK_ONLINE_GRID")) grid = std::max(1, std::min(cu_count(), atoi(e)));
+    s->onl_grid = grid;
+    s->online = true;
+    return TIK_OK;
+}
+
 static int record_step(tik_stream* s) {
+    if (s->online) {
+        HIP_TRY(tik::launch_online(s->onl_args.p, s->onl_grid, s->st));
+        return TIK_OK;
+    }
     HIP_TRY(hipMemcpyAsync(s->frame_in.p, s->host_frame, sizeof(float) * s->V * 3, hipMemcpyHostToDevice, s->st));
     HIP_TRY(tik::launch_stream_push(s->ring.p, s->W, s->V * 3, s->count.p, s->frame_in.p, s->st));
     HIP_TRY(tik::launch_stream_window(s->ring.p, s->W, s->V, s->count.p, s->h, 11, 12, 1, s->window.p, s->st));
@@ -73,10 +171,15 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
     if ((e = hipHostMalloc(&s->host_frame, sizeof(float) * s->V * 3, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s->host_pose, sizeof(float) * s->pose_dim, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s->host_pose, sizeof(float) * (s->pose_dim + 1), hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    s->host_pose[s->pose_dim] = 0.f;
     if ((e = hipMemsetAsync(s->count.p, 0, sizeof(int), s->st)) != hipSuccess) return bail("hipMemset", e);
     if ((e = hipMemsetAsync(s->ring.p, 0, sizeof(float) * s->W * s->V * 3, s->st)) != hipSuccess) return bail("hipMemset", e);
     if ((e = hipStreamSynchronize(s->st)) != hipSuccess) return bail("hipStreamSynchronize", e);
+    {
+        const char* env = getenv("TIK_ONLINE");
+        if (!(env && env[0] == '0') && setup_online(s) != TIK_OK) s->online = false;   // layered fallback
+    }
     if (use_graph) {
         if ((e = hipStreamBeginCapture(s->st, hipStreamCaptureModeThreadLocal)) != hipSuccess) return bail("hipStreamBeginCapture", e);
         rc = record_step(s);
@@ -94,6 +197,18 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
 int tik_stream_destroy(tik_stream_t s) {
     delete s;
     return TIK_OK;
+}
+
+int tik_stream_path(tik_stream_t s) {
+    if (!s) return fail(TIK_E_INVALID, "null stream");
+    return s->online ? 1 : 0;
+}
+
+int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap) {
+    if (!s || !s->online || !s->onl_trace.p) return fail(TIK_E_INVALID, "no online trace (TIK_ONLINE_TRACE=1 at tik_stream_create)");
+    const int n = std::min(cap / 8, s->onl_ntasks);
+    if (out && n > 0) HIP_TRY(hipMemcpy(out, s->onl_trace.p, sizeof(long long) * 8 * n, hipMemcpyDeviceToHost));
+    return s->onl_ntasks;
 }
 
 int tik_stream_reset(tik_stream_t s) {
@@ -114,6 +229,8 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
         if (rc) return rc;
     }
     HIP_TRY(hipStreamSynchronize(s->st));
+    if (s->online && s->host_pose[s->pose_dim] != 0.f)
+        return fail(TIK_E_HIP, "tik_stream_push: the online kernel timed out waiting on a dependency");
     ++s->pushed;
     const int valid = s->pushed > s->h;   // frame pushed-1-h >= 0 solved
     if (valid && pose_host) memcpy(pose_host, s->host_pose, sizeof(float) * s->pose_dim);

@@ -4,8 +4,10 @@ The reference is offline: `inference.run_inference` (inference.py:37-67)
 solves a recorded sequence with one edge-padded window per frame. Online,
 frame c is solvable once frame c+h has arrived (h = win_size//2); each
 `push` appends a frame to a device ring, gathers the window centred h frames
-back and runs the fused forward (N=1) as one hipGraph replay
-(`tik_stream_*`). Output for frame c is identical to run_inference's.
+back and solves it (`tik_stream_*`). Output for frame c is identical to
+run_inference's. The default step is one dataflow kernel (csrc/online.hip)
+over only the frames pose row 0 depends on, in fp32 (`path == "dataflow"`);
+TIK_ONLINE=0 selects the layered forward over the whole window.
 """
 from __future__ import annotations
 
@@ -35,6 +37,7 @@ class OnlineIK:
         self._destroy = lib.tik_stream_destroy
         self._pose = np.zeros(66, np.float32)
         self._last = None
+        self.path = "dataflow" if _lib.check(lib.tik_stream_path(self._s)) == 1 else "layered"
 
     def __del__(self):
         try:

@@ -7,8 +7,11 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("win,graph", [(64, True), (9, True), (9, False)])
-def test_stream_matches_run_inference(win, graph):
+@pytest.mark.parametrize("win,graph,online", [(64, True, "1"), (9, True, "1"), (9, False, "1"), (64, True, "0"),
+                                              (9, False, "0")])
+def test_stream_matches_run_inference(win, graph, online, monkeypatch):
+    """Both steps: the dataflow kernel (default) and the layered forward (TIK_ONLINE=0)."""
+    monkeypatch.setenv("TIK_ONLINE", online)
     from temporal_inverse_kinematics_amd import _build
     _build.build()
     from temporal_inverse_kinematics_amd.inference import run_inference, synthetic_model
@@ -18,6 +21,7 @@ def test_stream_matches_run_inference(win, graph):
     m = synthetic_model(win_size=win, device="cuda")
     ref = run_inference(m, seq)
     online = OnlineIK(m, use_graph=graph)
+    assert online.path == ("dataflow" if online_flag(online) else "layered")
     got = online.run(seq)
     assert got.shape == ref.shape
     assert np.abs(got - ref).max() < 1e-5
@@ -26,6 +30,53 @@ def test_stream_matches_run_inference(win, graph):
     # a second pass after reset gives the same answer
     again = online.run(seq)
     assert np.array_equal(again, got)
+
+
+def online_flag(_):
+    import os
+    return os.environ.get("TIK_ONLINE", "1") != "0"
+
+
+@pytest.mark.parametrize("win", [3, 21, 22, 23, 40, 64, 129])
+def test_online_kernel_matches_layered(win, monkeypatch):
+    """The dataflow step (only the frames pose row 0 depends on, fp32) against
+    the layered step on the whole window, over window sizes around the 22-frame
+    receptive field of row 0, including ones shorter than it."""
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    r = golden("run_inference.npz")
+    seq = r["seq"][:50]
+    m = synthetic_model(win_size=win, device="cuda")
+    monkeypatch.setenv("TIK_ONLINE", "0")
+    ref = OnlineIK(m, use_graph=True).run(seq)
+    monkeypatch.setenv("TIK_ONLINE", "1")
+    s = OnlineIK(m, use_graph=True)
+    assert s.path == "dataflow"
+    got = s.run(seq)
+    assert np.abs(got - ref).max() < 2e-5
+    # 300 more replays: counters and tickets are left clean by every launch
+    for i in range(300):
+        s.push(seq[i % seq.shape[0]])
+    assert np.array_equal(s.run(seq), got)
+
+
+@pytest.mark.parametrize("grid", ["1", "3", "64"])
+def test_online_kernel_grid_sizes(grid, monkeypatch):
+    """Any number of workgroups gives the same poses (tickets are taken in
+    topological order, so even one workgroup runs every task)."""
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    r = golden("run_inference.npz")
+    seq = r["seq"][:40]
+    m = synthetic_model(win_size=64, device="cuda")
+    base = OnlineIK(m, use_graph=False).run(seq)
+    monkeypatch.setenv("TIK_ONLINE_GRID", grid)
+    got = OnlineIK(m, use_graph=True).run(seq)
+    assert np.array_equal(got, base)
 
 
 def test_stream_survives_batch_calls_and_rebuilds():

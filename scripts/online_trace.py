@@ -29,7 +29,6 @@ def main():
     buf = (ctypes.c_longlong * (8 * n))()
     lib.tik_debug_stream_trace(s._s, buf, 8 * n)
     tr = np.frombuffer(buf, dtype=np.int64).reshape(n, 8).astype(np.float64)
-    tr[0, 1] = tr[0, 0]
     t0 = tr[:, 0].min()
     us = (tr[:, :7] - t0) / 100.0   # 100 MHz ticks -> us
     # phase table (stream.cpp setup_online)
@@ -45,7 +44,7 @@ def main():
         nout[l] = need
         nin[l] = min(tin[l], strides[l] * (need - 1) + 2)
         need = nin[l]
-    phases = [("INPUT", 1)]
+    phases = []
     for l in range(8):
         phases += [(f"G{l}", nin[l] * couts[l] // 16), (f"T{l}", nout[l] * couts[l] // 16)]
     phases += [("H0", 512 // 16), ("H1", (66 + 15) // 16)]

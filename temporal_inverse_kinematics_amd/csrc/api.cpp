@@ -428,7 +428,30 @@ struct Layer {
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
             p.out(z, (size_t)rin * ldz * 2);
+            static const bool gtrace = getenv("TIK_G_TRACE") != nullptr;   // debug: per-workgroup loop / epilogue time
+            const int nwg = (int)((rin + 271) / 272) * ((cout + (wide ? 127 : 63)) / (wide ? 128 : 64));
+            unsigned long long* d = nullptr;
+            if (gtrace) {
+                HIP_TRY(hipMalloc(&d, (size_t)nwg * 5 * 8));
+                g.trace = d;
+            }
             HIP_TRY(tik::launch_cgemm3(g, wide ? tik::C3_G272x128_W8 : tik::C3_G272x64, st));
+            if (gtrace) {
+                HIP_TRY(hipStreamSynchronize(st));
+                std::vector<unsigned long long> h((size_t)nwg * 5);
+                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipFree(d));
+                double loop = 0, epi = 0, vmw = 0;
+                unsigned long long lo = ~0ull, hi = 0;
+                for (int w = 0; w < nwg; ++w) {
+                    loop += (double)(h[5 * w + 1] - h[5 * w]);
+                    epi += (double)(h[5 * w + 2] - h[5 * w + 1]);
+                    vmw += (double)h[5 * w + 3];
+                    lo = std::min(lo, h[5 * w]); hi = std::max(hi, h[5 * w + 2]);
+                }
+                fprintf(stderr, "G L%d (%d wg): per-wg us loop %.2f epilogue %.2f (wave0 DMA wait %.0f cycles) | span %.1f us\n",
+                        index, nwg, loop / nwg / 100, epi / nwg / 100, vmw / nwg, (hi - lo) / 100.0);
+            }
         }
         tik::Cgemm3Args t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;

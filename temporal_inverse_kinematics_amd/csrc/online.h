@@ -7,9 +7,10 @@
 // 2, 4, 8, 9, 10, 20, 21, 22 input frames for the IK net at any window of at
 // least 22 frames). The step computes exactly those frames, in fp32 VALU
 // arithmetic, as a list of small tasks in topological order:
-//   INPUT: ring append of the new frame (read from pinned host memory),
-//          window gather (left-edge clamp), root-relative, data_bn
-//   G_L(f, 16 channels): gcn 1x1 conv + 17x17 graph mix + bias + ReLU
+//   G_L(f, 16 channels): gcn 1x1 conv + 17x17 graph mix + bias + ReLU (layer 0
+//          builds its input rows itself: window gather with the left-edge
+//          clamp, root-relative, data_bn; the pushed frame is read from pinned
+//          host memory and appended to the ring by the launch's last workgroup)
 //   T_L(t, 16 channels): 3x1 temporal conv + residual + bias + ReLU
 //   H0(16 hidden units), H1(16 pose values, written straight to pinned host memory)
 // Workgroups take task tickets in order and wait only on per-frame completion
@@ -23,7 +24,7 @@ namespace tik {
 constexpr int ONL_MAXL = 12;        // layers
 constexpr int ONL_MAXC = 256;       // channels per layer
 constexpr int ONL_MAXHC = 20;       // head K chunks of 4 per lane: K <= 20 * 4 * 64 = 5120
-enum { ONP_INPUT = 0, ONP_G = 1, ONP_T = 2, ONP_H0 = 3, ONP_H1 = 4 };
+enum { ONP_G = 1, ONP_T = 2, ONP_H0 = 3, ONP_H1 = 4 };
 enum { ONR_ZERO = 0, ONR_IDEN = 1, ONR_CONV = 2 };
 
 struct OnlineLayer {
@@ -31,7 +32,7 @@ struct OnlineLayer {
     int tin;           // the layer's real input frame count (zero padding past it)
     int n_in, n_out;   // frames computed: z (gcn) / out (temporal conv)
     const float *wg, *bias2, *amix, *wt, *wr, *biasT;   // the fp32 folded weights of api.cpp's Layer
-    const float* x;    // input rows [n_in][17][cinp]
+    const float* x;    // input rows [n_in][17][cinp] (layer 0: built in place from the ring)
     float *z, *out;    // [n_in][17][cout], [n_out][17][cout]
 };
 
@@ -49,7 +50,6 @@ struct OnlineArgs {
     int* count;
     const float* frame;   // the pushed frame (pinned host memory)
     const float *bn_sc, *bn_sh;
-    float* x0;            // [n_in0][17][4]
     // head
     const float *w0, *b0, *w3, *b3;
     int feat, hidden, pose_dim;
@@ -63,7 +63,7 @@ struct OnlineArgs {
     int ncnt;
     int* err;             // sticky: a dependency wait timed out
     unsigned long long* trace;   // debug (TIK_ONLINE_TRACE=1): per task {grab, inputs ready, done, workgroup}
-    float* act;           // the one buffer every inter-task activation lives in (x0, z, out, hid)
+    float* act;           // the one buffer every inter-task activation lives in (z, out, hid)
     unsigned act_bytes;
 };
 

@@ -99,32 +99,27 @@ __device__ __forceinline__ float fma4(const float4 a, const float4 b, float c) {
     return fmaf(a.w, b.w, c);
 }
 
-// ---- INPUT: ring append + window gather + root-relative + data_bn (online.h)
-__device__ void onl_input(const OnlineArgs* __restrict__ A, const OnlinePhase& ph, int task) {
-    const int tid = threadIdx.x;
-    const int c = cnt_load(A->count);   // frames pushed before this one
-    const int W = A->W, nv = 17 * 3;
-    const float* __restrict__ fr = A->frame;
-    float* slot = A->ring + (size_t)(c % W) * nv;
-    for (int i = tid; i < nv; i += onl::NT) slot[i] = fr[i];
-    const int n0 = A->L[0].n_in, last = c, ra = A->ra, rb = A->rb, rel = A->relative;
-    const Act ab = act_of(A);
-    for (int p = tid; p < n0 * 17; p += onl::NT) {
-        const int k = p / 17, v = p - 17 * k;
-        int fi = last - 2 * A->h + k;
-        fi = fi < 0 ? 0 : fi;
-        const float* src = fi == last ? fr : A->ring + (size_t)(fi % W) * nv;
-        float o[3];
+// ---- the layer-0 input rows of window frame k, computed where they are used
+// (no input task, no round trip): window gather with the left-edge clamp,
+// root-relative, data_bn -> 17 rows of 4 floats at dst (threads 0-16).
+// The pushed frame is read from pinned host memory; older frames from the ring,
+// which the last workgroup of the launch appends the pushed frame to.
+__device__ void onl_raw_rows(const OnlineArgs* __restrict__ A, int k, float4* dst) {
+    const int v = threadIdx.x;
+    if (v >= 17) return;
+    const int last = cnt_load(A->count);   // frames pushed before this one = the pushed frame's index
+    const int W = A->W, nv = 17 * 3, ra = A->ra, rb = A->rb;
+    int fi = last - 2 * A->h + k;
+    fi = fi < 0 ? 0 : fi;
+    const float* src = fi == last ? A->frame : A->ring + (size_t)(fi % W) * nv;
+    float o[3];
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            float x = src[v * 3 + e];
-            if (rel) x -= 0.5f * (src[ra * 3 + e] + src[rb * 3 + e]);
-            o[e] = fmaf(x, A->bn_sc[v * 3 + e], A->bn_sh[v * 3 + e]);
-        }
-        st4c(ab, A->x0 + 4 * p, make_float4(o[0], o[1], o[2], 0.f));
+    for (int e = 0; e < 3; ++e) {
+        float x = src[v * 3 + e];
+        if (A->relative) x -= 0.5f * (src[ra * 3 + e] + src[rb * 3 + e]);
+        o[e] = fmaf(x, A->bn_sc[v * 3 + e], A->bn_sh[v * 3 + e]);
     }
-    if (tid == 0) A->count[0] = c + 1;
-    onl_release(A, ph.cbase, task);
+    dst[v] = make_float4(o[0], o[1], o[2], 0.f);
 }
 
 // Thread roles of a G / T task: 1024 threads = 16 output channels (co = tid & 15)
@@ -163,7 +158,6 @@ __device__ __forceinline__ void onl_reduce17(float (&acc)[17], float* sm) {
 // ---- G_L(f, 16 channels): z = ReLU(bias2 + sum_v A[v][w] (x . wg^T)[v])
 __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task) {
     const OnlinePhase& ph = A->ph[p];
-    const OnlinePhase& pp = A->ph[p - 1];
     const OnlineLayer& L = A->L[ph.layer];
     const int tid = threadIdx.x, co = tid & 15, ks = tid >> 4;
     const int f = idx / ph.ngroups, cg = idx - f * ph.ngroups;
@@ -182,14 +176,21 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
 #pragma unroll
     for (int v = 0; v < 17; ++v) onl_hold(am[v]);
     if (tid == 0) {
-        onl_wait(A, pp.cbase + (pp.kind == ONP_INPUT ? 0 : f), pp.ngroups);
+        if (ph.layer > 0) {   // the previous temporal conv's frame f
+            const OnlinePhase& pp = A->ph[p - 1];
+            onl_wait(A, pp.cbase + f, pp.ngroups);
+        }
         onl_mark(A, task, 1);
     }
     __syncthreads();
     float4* s4 = reinterpret_cast<float4*>(sm);
     const Act ab = act_of(A);
-    const float* xr = L.x + (size_t)f * 17 * cinp;
-    for (int i = tid; i < 17 * K4; i += onl::NT) s4[i] = ld4c(ab, xr + 4 * i);
+    if (ph.layer == 0) {
+        onl_raw_rows(A, f, s4);
+    } else {
+        const float* xr = L.x + (size_t)f * 17 * cinp;
+        for (int i = tid; i < 17 * K4; i += onl::NT) s4[i] = ld4c(ab, xr + 4 * i);
+    }
     __syncthreads();
     if (tid == 0) onl_mark(A, task, 2);
     float acc[17];
@@ -250,7 +251,9 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     float4* xs4 = s4 + 3 * nz;
     const float* xs = reinterpret_cast<const float*>(xs4);
     const float* xrow = L.x + (size_t)fx * 17 * L.cinp;
-    if (L.res != ONR_ZERO)   // residual rows: the conv's K segment, or the identity term
+    if (ph.layer == 0 && L.res != ONR_ZERO)
+        onl_raw_rows(A, fx, xs4);
+    else if (L.res != ONR_ZERO)   // residual rows: the conv's K segment, or the identity term
         for (int i = tid; i < 17 * cinp4; i += onl::NT) xs4[i] = ld4c(ab, xrow + 4 * i);
     __syncthreads();
     if (tid == 0) onl_mark(A, task, 2);
@@ -350,7 +353,6 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
         while (p + 1 < A->nph && task >= A->ph[p + 1].task0) ++p;
         const int idx = task - A->ph[p].task0;
         switch (A->ph[p].kind) {
-            case ONP_INPUT: onl_input(A, A->ph[p], task); break;
             case ONP_G: onl_gcn(A, p, idx, sm, task); break;
             case ONP_T: onl_tconv(A, p, idx, sm, task); break;
             case ONP_H0: onl_head<true>(A, p, idx, sm, task); break;
@@ -367,7 +369,11 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
     __syncthreads();
     if (s_last) {
         for (int i = tid; i < A->ncnt; i += onl::NT) A->cnt[i] = 0;
+        // every task has read the ring and the count: append the pushed frame
+        const int c = cnt_load(A->count);
+        for (int i = tid; i < 17 * 3; i += onl::NT) A->ring[(size_t)(c % A->W) * 17 * 3 + i] = A->frame[i];
         if (tid == 0) {
+            A->count[0] = c + 1;
             A->ticket[0] = 0;
             A->done[0] = 0;
         }

@@ -79,14 +79,13 @@ static int setup_online(tik_stream* s) {
         L.n_in = std::min(L.tin, L.stride * (need - 1) + 2);
         need = L.n_in;
     }
-    size_t tot = (size_t)a.L[0].n_in * 17 * 4 + a.hidden + ((a.pose_dim + 3) & ~3);
+    size_t tot = (size_t)a.hidden + ((a.pose_dim + 3) & ~3);
     for (int l = 0; l < nl; ++l) tot += (size_t)(a.L[l].n_in + a.L[l].n_out) * 17 * a.L[l].cout;
     if ((rc = s->onl_act.reserve(tot))) return rc;
     float* q = s->onl_act.p;
-    a.x0 = q; q += (size_t)a.L[0].n_in * 17 * 4;
     for (int l = 0; l < nl; ++l) {
         tik::OnlineLayer& L = a.L[l];
-        L.x = l == 0 ? a.x0 : a.L[l - 1].out;
+        L.x = l == 0 ? nullptr : a.L[l - 1].out;
         L.z = q; q += (size_t)L.n_in * 17 * L.cout;
         L.out = q; q += (size_t)L.n_out * 17 * L.cout;
     }
@@ -100,7 +99,6 @@ static int setup_online(tik_stream* s) {
         task += nf * ng;
         cb += nf;
     };
-    add(tik::ONP_INPUT, 0, 1, 1);
     for (int l = 0; l < nl; ++l) {
         add(tik::ONP_G, l, a.L[l].n_in, a.L[l].cout / 16);
         add(tik::ONP_T, l, a.L[l].n_out, a.L[l].cout / 16);

@@ -331,7 +331,8 @@ struct Layer {
     int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
                  bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
                  const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true, const Layer* nxt = nullptr,
-                 half_t* znext = nullptr, bool zready = false, half_t* trash = nullptr) const {
+                 half_t* znext = nullptr, bool zready = false, half_t* trash = nullptr,
+                 half_t* gtrash = nullptr) const {
         const int ldz = 64 * sbt.nblk;
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
@@ -422,6 +423,38 @@ struct Layer {
             HIP_TRY(tik::launch_gcn0(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
                                      cout, z, ldz, xb4, st));
         } else {
+            g.trash = gtrash;
+            if (gtrash && tik::gpw_ok(g)) {
+                // weight-stationary persistent gcn: the next tile's x streams in behind this one (gpw.hip)
+                const std::string lab = std::string("GP_") + std::to_string(cout) + ".L" + std::to_string(index);
+                ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                            4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+                p.out(z, (size_t)rin * ldz * 2);
+                static const bool gtr = getenv("TIK_G_TRACE") != nullptr;   // debug: per-tile phase timing
+                unsigned long long* d = nullptr;
+                if (gtr) {
+                    HIP_TRY(hipMalloc(&d, (size_t)1024 * 8 * 8));
+                    HIP_TRY(hipMemset(d, 0, (size_t)1024 * 8 * 8));
+                    g.trace = d;
+                }
+                HIP_TRY(tik::launch_gpw(g, st));
+                if (gtr) {
+                    HIP_TRY(hipStreamSynchronize(st));
+                    std::vector<unsigned long long> h((size_t)1024 * 8);
+                    HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+                    HIP_TRY(hipFree(d));
+                    double ph[6] = {0, 0, 0, 0, 0, 0}, tiles = 0;
+                    for (int w = 0; w < 1024; ++w) {
+                        tiles += (double)h[8 * w];
+                        for (int k = 0; k < 6; ++k) ph[k] += (double)h[8 * w + 1 + k];
+                    }
+                    tiles = std::max(1.0, tiles);
+                    fprintf(stderr, "GP L%d (%.0f tiles): per-tile us wait %.2f (issue %.2f, vmcnt %.2f) mfma %.2f y-stage %.2f mix+stores %.2f\n",
+                            index, tiles, ph[0] / tiles / 100, ph[4] / tiles / 100, ph[5] / tiles / 100, ph[1] / tiles / 100,
+                            ph[2] / tiles / 100, ph[3] / tiles / 100);
+                }
+                goto temporal;
+            }
             // 128-column tiles (8 waves) read each input row once per 128 outputs
             const bool wide = cout % 128 == 0;
             const std::string lab = std::string(wide ? "G3_272x128.L" : "G3_272x64.L") + std::to_string(index);
@@ -453,6 +486,7 @@ struct Layer {
                         index, nwg, loop / nwg / 100, epi / nwg / 100, vmw / nwg, (hi - lo) / 100.0);
             }
         }
+    temporal:
         tik::Cgemm3Args t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
         t.seg[0] = mkseg3(z, ldz, sbt, TK, stride, 1, tin);
@@ -588,6 +622,7 @@ struct tik_model {
     bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
     bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
     bool tgw = true;                   // stride-1 fused blocks on the weight-stationary kernel (TIK_TGW=0: TG3)
+    bool gpw = true;                   // unfused gcn launches on the persistent kernel (TIK_GPW=0: G3_272x128)
     DevHBuf trash;                     // scratch line for the tgw kernel's stores of invalid rows
     Profiler prof;
     bool profiling = false;
@@ -721,6 +756,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
     if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
+    if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
@@ -894,7 +930,8 @@ static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t**
         const Layer* nxt = (m->fuse_tg && li + 1 < m->layers.size() && L.can_fuse_next(m->layers[li + 1]))
                                ? &m->layers[li + 1] : nullptr;
         if ((rc = L.forward3(cur, ld, N, t, zb[zi], o, m->zeros.p, st, false, raw ? x : nullptr, m->bn_sc.p,
-                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready, m->tgw ? m->trash.p : nullptr)))
+                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready, m->tgw ? m->trash.p : nullptr,
+                             m->gpw ? m->trash.p : nullptr)))
             return rc;
         zready = nxt != nullptr;
         if (nxt) zi ^= 1;

@@ -90,6 +90,11 @@ hipError_t launch_tgemm(const Cgemm3Args& a, int cfg, hipStream_t st);
 bool tgw_ok(const Cgemm3Args& a);
 hipError_t launch_tgw(const Cgemm3Args& a, hipStream_t st);
 
+// weight-stationary persistent gcn (gpw.hip, GP_*): 1x1 conv + graph mix + bias +
+// ReLU for 64->128, 128->256, 256->256, V = 17; the next tile's x DMA'd behind the current
+bool gpw_ok(const Cgemm3Args& a);
+hipError_t launch_gpw(const Cgemm3Args& a, hipStream_t st);
+
 // stride-1 temporal conv + residual with a frame halo in LDS (tconv.hip):
 // seg[0] kt=3/stride 1/pad 1, optional seg[1] kt=1 (residual conv), V=17,
 // Nc % 64 == 0; bn = 64 or 128 output columns per tile

@@ -350,3 +350,23 @@ def test_weight_stationary_tgw_bitwise():
             assert torch.equal(y, tg3(x)["poses"]), (n, T)
             assert torch.equal(y, plain(x)["poses"]), (n, T)
 
+
+
+def test_persistent_gcn_gpw_bitwise():
+    """The unfused gcn launches (L2 64->128, L6 128->256, L7 256->256) on the
+    weight-stationary persistent kernel (gpw.hip, GP_*) give poses
+    bit-identical to the G3_272x128 tiles (TIK_GPW=0): same f16x3 products in
+    the same K order, same mix order. With TIK_FUSE_TG=0 every block's gcn goes
+    through it (128->128 is not a gpw shape there, so L3-L5 stay on G3).
+    Batches: the bench size, a ragged one, T=65 windows, fewer tiles than CUs."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    gpw = _model_with_env(TIK_SPLIT=0)
+    g3 = _model_with_env(TIK_GPW=0, TIK_SPLIT=0)
+    gpw_l = _model_with_env(TIK_FUSE_TG=0, TIK_SPLIT=0)
+    g3_l = _model_with_env(TIK_FUSE_TG=0, TIK_GPW=0, TIK_SPLIT=0)
+    for n, T in [(1024, 64), (333, 64), (70, 65), (3, 64), (1, 9)]:
+        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 5)).cuda()
+        with torch.no_grad():
+            y = gpw(x)["poses"]
+            assert torch.equal(y, g3(x)["poses"]), (n, T)
+            assert torch.equal(gpw_l(x)["poses"], g3_l(x)["poses"]), (n, T)

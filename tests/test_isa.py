@@ -78,3 +78,44 @@ def test_fk_skin_loop_memory_instruction_counts(tmp_path):
     assert c == Counter({"buffer_load_dwordx4": 8, "global_load_dwordx3": 16, "global_load_dword": 8,
                          "global_store_dword": 16}), c
 
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_gpw_loop_memory_instruction_counts(tmp_path):
+    """The persistent gcn kernel (csrc/gpw.hip) waits for each tile's x image
+    with one exact vmcnt count per tile (younger: the next tile's x DMAs and the
+    previous tile's line stores), so per tile and wave it must issue exactly
+    NIW LDS-DMA instructions and NSP whole-line stores, and nothing else."""
+    src = os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", "gpw.hip")
+    out = tmp_path / "gpw.s"
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
+                        "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    lines = out.read_text().split("\n")
+    # <CIN, COUT, FT, NW, NBUF> -> (DMA instructions per wave, line stores per thread)
+    want = {(64, 128, 4, 4, 1): (5, 9), (64, 128, 8, 8, 2): (5, 9), (128, 256, 3, 8, 2): (4, 7)}
+    seen = set()
+    for i, l in enumerate(lines):
+        m = re.match(r"^_ZN3tik10gpw_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)EEEvNS_10Cgemm3ArgsEi:", l)
+        if not m:
+            continue
+        key = tuple(int(x) for x in m.groups())
+        en = next(j for j in range(i, len(lines)) if "s_endpgm" in lines[j])
+        body = lines[i:en]
+        hdr = [re.match(r"^\.(LBB\d+_\d+):", b).group(1) for b in body if "Loop Header: Depth=1" in b]
+        best = None
+        for h in hdr:
+            idx = [k for k, b in enumerate(body) if f"Header={h[1:]} " in b + " " or b.startswith(f".{h}:")]
+            lo, hi = min(idx), max(idx)
+            j = hi + 1
+            while j < len(body) and not re.match(r"^\.LBB\d+_\d+:", body[j]):
+                j += 1
+            nm = sum("v_mfma" in b for b in body[lo:j])
+            if nm > (best[0] if best else 0):
+                best = (nm, body[lo:j])
+        assert best, key
+        c = Counter(mm.group(1) for b in best[1] for mm in [re.match(r"\s+((?:global|buffer|scratch|flat)_\w+)", b)] if mm)
+        ndma, nst = want[key]
+        assert c == Counter({"buffer_load_dwordx4": ndma, "global_store_dwordx4": nst}), (key, c)
+        seen.add(key)
+    assert seen == set(want), seen

@@ -119,7 +119,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     from temporal_inverse_kinematics_amd import _build, _lib, synthetic as syn
-    from temporal_inverse_kinematics_amd.distributed import gather_poses
+    from temporal_inverse_kinematics_amd.distributed import PosesGatherPipeline
     from temporal_inverse_kinematics_amd.inference import synthetic_model
     if rank == 0:
         _build.build()
@@ -133,15 +133,20 @@ def main():
     Tp = reg.backbone.out_frames(T)
     full = torch.empty((world * B, Tp, 66), device=dev) if world > 1 else None
 
+    # the all-gather of step k runs on RCCL's stream while step k+1's forward
+    # runs (PosesGatherPipeline); every gather is waited on inside the timed region
+    gathers = PosesGatherPipeline()
+
     def step():
         y = reg(x)["poses"]
         if world > 1:
-            gather_poses(y, full)
+            gathers.push(y, full)
         return y
 
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
+        gathers.drain()
         lib = _lib.load()
         h = reg.tik_handle()
         per_fwd = 2 * len(reg.backbone.st_gcn_networks) + 3
@@ -154,6 +159,7 @@ def main():
             t0 = time.perf_counter()
             for _ in range(k):
                 step()
+            gathers.drain()
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()

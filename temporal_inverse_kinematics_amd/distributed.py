@@ -53,3 +53,41 @@ def sharded_forward(forward: Callable[[torch.Tensor], torch.Tensor], windows: to
     full = gather_poses(pad)
     parts = [full[r * cap: r * cap + (shard_range(n, r, world)[1] - shard_range(n, r, world)[0])] for r in range(world)]
     return torch.cat(parts, 0)
+
+
+class PosesGatherPipeline:
+    """Overlaps the pose all-gather of batch k with the forward of batch k+1.
+
+    push(y) issues the all-gather of this rank's block y asynchronously (RCCL
+    runs it on its own stream after the forward that produced y) into `out`
+    (or a fresh (world*B,...) tensor) and then makes the caller's stream wait
+    for the PREVIOUS batch's gather, so that gather ran concurrently with this
+    batch's forward. drain() waits for the last one. Each gathered tensor is
+    complete once the next push() (or drain()) has returned; push returns the
+    tensor its gather writes. The local blocks stay referenced until their
+    gather is waited on."""
+
+    def __init__(self):
+        self._pending = []
+
+    def push(self, local: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return local if out is None else out.copy_(local)
+        world = dist.get_world_size()
+        if out is None:
+            out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+        local = local.contiguous()
+        if dist.get_backend() == "gloo":
+            work = dist.all_gather(list(out.chunk(world, 0)), local, async_op=True)
+        else:
+            work = dist.all_gather_into_tensor(out, local, async_op=True)
+        self._pending.append((work, local, out))
+        while len(self._pending) > 1:
+            w, _, _ = self._pending.pop(0)
+            w.wait()
+        return out
+
+    def drain(self) -> None:
+        while self._pending:
+            w, _, _ = self._pending.pop(0)
+            w.wait()

@@ -107,3 +107,34 @@ def test_empty_batch_forward_cpu():
     assert tuple(y.shape) == (0, 4, 66)
     f = m.backbone_features(torch.zeros((0, 9, 17, 3)))
     assert tuple(f.shape) == (0, 1, 17 * 256)
+
+
+def _pipe_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from temporal_inverse_kinematics_amd.distributed import PosesGatherPipeline, gather_poses
+    pipe = PosesGatherPipeline()
+    outs, refs = [], []
+    for k in range(4):
+        y = torch.full((3, 4, 66), float(10 * k + rank))
+        refs.append(gather_poses(y))
+        outs.append(pipe.push(y))
+    pipe.drain()
+    ok = all(torch.equal(a, b) for a, b in zip(outs, refs))
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_gather_pipeline_gloo_ws2():
+    """The overlapped all-gather (bench.py's multi-GPU step) delivers every
+    batch's gathered poses, in rank order, once the next push / drain returns."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: True, 1: True}

@@ -166,6 +166,27 @@ int tik_stream_path(tik_stream_t s);
 int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap);
 
 /* ------------------------------------------------------------------------
+ * Training-data generation (data half): AmassDataset
+ * (mmskeleton/datasets/data_amass.py:87-218) on the GPU.
+ * tik_rotate_root_z: regenerate_data's root-orientation augmentation
+ * (:184-190) in place on pose rows (ld floats, first 3 = root axis-angle):
+ * rotvec(R_z(angle) R(root)), float64 as scipy's Rotation does it.
+ * tik_train_windows: __getitem__ (:125-154) for B items: edge-padded window
+ * (2h+1 frames, h <= 64) of the FK joints [rows][n_joints][3] -> COCO-17
+ * (coco_map, host) -> root-relative -> per-joint Gaussian noise (sigma, host:
+ * coco_kps_sigma) -> windows [B][2h+1][17][3]; target = pose row of the
+ * window's last frame, first 66 values -> [B][66]. Items (device int arrays):
+ * sequence start row, sequence length, window centre, dataset index (the
+ * noise stream: counter-based, keyed by (seed, index)). The caller checks the
+ * reference's ValueError / short-window cases (the Python layer does).
+ * ---------------------------------------------------------------------- */
+int tik_rotate_root_z(float* poses, int F, int ld, double angle, void* stream);
+int tik_train_windows(const float* joints, int n_joints, const float* poses, int pose_ld, const int* item_start,
+                      const int* item_len, const int* item_idx, const int* item_uid, int B, int h,
+                      const int* coco_map, const float* sigma, int relative, int add_noise, unsigned long long seed,
+                      float* windows, float* target, void* stream);
+
+/* ------------------------------------------------------------------------
  * SMPL-X forward kinematics + linear blend skinning (the FK check).
  * Replaces common/smpl_util.py:8-82 (load_smplx_models / run_smpl_inference)
  * and the third-party smplx.SMPLX.forward it calls (smpl_util.py:67-69;

@@ -59,6 +59,8 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_stream_reset": (_I, (_P,)),
     "tik_stream_push": (_I, (_P, _F, _F)),
     "tik_stream_path": (_I, (_P,)),
+    "tik_rotate_root_z": (_I, (_P, _I, _I, ctypes.c_double, _P)),
+    "tik_train_windows": (_I, (_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _I, ctypes.c_ulonglong, _P, _P, _P)),
     "tik_debug_stream_trace": (_I, (_P, ctypes.POINTER(ctypes.c_longlong), _I)),
     "tik_fk_create": (_I, (ctypes.POINTER(TikTensor), _I, _I, ctypes.POINTER(_P))),
     "tik_fk_destroy": (_I, (_P,)),

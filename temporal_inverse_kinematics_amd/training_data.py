@@ -16,7 +16,7 @@ root-relative, with per-joint Gaussian noise, plus the target pose row;
 Noise: the reference samples np.random.multivariate_normal from numpy's
 global state; here the same distribution comes from a counter-based generator
 keyed by (noise_seed, epoch, dataset index), so batches are reproducible and
-independent of how items are grouped (oracle/amass.py restates it).
+independent of how items are grouped (the tests restate it on the CPU).
 """
 from __future__ import annotations
 
@@ -186,7 +186,7 @@ class AmassDataset(torch.utils.data.Dataset):
 
     @property
     def noise_key(self) -> int:
-        """The noise generator's seed for this epoch (oracle/amass.py counter_normal)."""
+        """The noise generator's seed for this epoch (train_data.hip counter_normal)."""
         return (self.noise_seed * 1000003 + self.epoch) & 0xFFFFFFFFFFFFFFFF
 
     # ---------------------------------------------------------------- items

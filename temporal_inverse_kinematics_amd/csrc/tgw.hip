@@ -21,8 +21,9 @@
 //
 // Persistent: one 512-thread workgroup per CU walks a contiguous run of tiles
 // (runs laid out per XCD). The four block slots of the NEXT tile are DMA'd as
-// soon as the current tile's last tap has read them, and its residual tile x
-// right after the epilogue, so HBM keeps streaming through the epilogue.
+// soon as every wave is past the current tile's last tap (the epilogue's first
+// barrier), and its residual tile x in tap 0, so HBM keeps streaming through
+// the epilogue.
 // Every wave issues a fixed number of vector-memory instructions per tile
 // (slot DMA, residual DMA, 8 gcn-weight loads, 8 + 8 whole-line stores;
 // invalid rows go to a trash line), which makes every counted vmcnt wait
@@ -253,6 +254,10 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         for (int kb = 0; kb < 4; ++kb) asm volatile("" : "+v"(wgh[kb]), "+v"(wgl[kb]));
         const unsigned long long tsw = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         lds_barrier();   // ... for every wave; and every wave is done with the four slots
+        // the next tile's four blocks stream in behind the whole epilogue (issued
+        // inside the next-gcn loop they landed later: TW 0.359 -> 0.353 ms)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) issue_slot(kb);
         const unsigned long long tsb = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         // (2) out = ReLU(C + bias + x) -> the split image of out, IN PLACE of the residual
         // image: each (pixel, 4-channel) piece is read and rewritten by the same lane
@@ -300,7 +305,6 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
             load_g(1);
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb) {
-                issue_slot(kb);   // the next tile's block kb streams in behind the epilogue
 #pragma unroll
                 for (int i = 0; i < NPF; ++i) {
                     const int n = kb * NPF + i;

@@ -32,6 +32,7 @@
 // Arithmetic is cgemm3/tgemm's f16x3 (a_lo b_hi + a_hi b_lo + a_hi b_hi, fp32
 // accumulate) in the same K order, and the mix adds bias2' then the joints in
 // order, like the TG_128x128_G7 epilogue it replaces.
+#include <cstdlib>
 #include <type_traits>
 
 #include "cgemm3_dev.h"
@@ -56,6 +57,7 @@ static_assert(RT * LDY * 4 <= 4 * EB, "Y fits the E region");
 static_assert(SMEM <= 160 * 1024, "LDS");
 }  // namespace tw
 
+template <int PD>
 __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
     using namespace tw;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];   // the only LDS object
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         // wave is past the last epilogue's reads of the E region (the residual DMA target)
         wait_vm_dyn(prev_stores);
         lds_barrier();
-        // K loop, fully unrolled over (tap, block, fragment) with the B reads two
+        // K loop, fully unrolled over (tap, block, fragment) with the B reads PD
         // fragments ahead of their MFMAs (a read consumed right away exposes the
         // LDS latency; measured: loop at ~2x the MFMA time)
         f16x8 wgh[4], wgl[4];
@@ -197,7 +199,6 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         };
         tap_offsets(0, bo[0]);
         constexpr int NSTEP = 3 * 4 * NPF;   // (tap, block, fragment) triples
-        constexpr int PD = 2;                // prefetch distance
         f16x8 pbh[PD + 1], pbl[PD + 1];
         auto load_b = [&](int n) {
             const int tap = n / (4 * NPF), blk = (n / NPF) % 4, i = n % NPF;
@@ -449,7 +450,8 @@ hipError_t launch_tgw(const Cgemm3Args& a, hipStream_t st) {
     const int ntiles = (a.M / 17 + tw::FG - 1) / tw::FG;
     const int grid = ntiles < cu_count() ? ntiles : cu_count();
     (void)hipGetLastError();
-    hipLaunchKernelGGL(tgw_kernel, dim3(grid), dim3(512), 0, st, a, ntiles);
+    // B operand reads three fragments ahead of their MFMAs (measured: two ahead 0.355 ms, three 0.352 ms)
+    hipLaunchKernelGGL(tgw_kernel<3>, dim3(grid), dim3(512), 0, st, a, ntiles);
     return hipGetLastError();
 }
 

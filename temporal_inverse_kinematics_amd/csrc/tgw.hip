@@ -57,7 +57,7 @@ static_assert(RT * LDY * 4 <= 4 * EB, "Y fits the E region");
 static_assert(SMEM <= 160 * 1024, "LDS");
 }  // namespace tw
 
-template <int PD>
+template <int PD, int PG>
 __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
     using namespace tw;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];   // the only LDS object
@@ -295,22 +295,22 @@ __global__ __launch_bounds__(512, 2) void tgw_kernel(Cgemm3Args a, int ntiles) {
         for (int i = 0; i < NPF; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         {
             // B reads two fragments ahead of their MFMAs, as in the K loop
-            f16x8 gbh[3], gbl[3];
+            f16x8 gbh[PG + 1], gbl[PG + 1];
             auto load_g = [&](int n) {
                 const unsigned char* B = smem + EOFF + (n / NPF) * EB;
                 const int p = 16 * (n % NPF) + l15;
-                gbh[n % 3] = *reinterpret_cast<const f16x8*>(B + sbo(p, g));
-                gbl[n % 3] = *reinterpret_cast<const f16x8*>(B + sbo(p, 4 + g));
+                gbh[n % (PG + 1)] = *reinterpret_cast<const f16x8*>(B + sbo(p, g));
+                gbl[n % (PG + 1)] = *reinterpret_cast<const f16x8*>(B + sbo(p, 4 + g));
             };
-            load_g(0);
-            load_g(1);
+#pragma unroll
+            for (int n = 0; n < PG; ++n) load_g(n);
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
                 for (int i = 0; i < NPF; ++i) {
                     const int n = kb * NPF + i;
-                    if (n + 2 < 4 * NPF) load_g(n + 2);
-                    const f16x8 bh = gbh[n % 3], bl = gbl[n % 3];
+                    if (n + PG < 4 * NPF) load_g(n + PG);
+                    const f16x8 bh = gbh[n % (PG + 1)], bl = gbl[n % (PG + 1)];
                     acc2[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[kb], bl, acc2[i], 0, 0, 0);
                     acc2[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgl[kb], bh, acc2[i], 0, 0, 0);
                     acc2[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wgh[kb], bh, acc2[i], 0, 0, 0);
@@ -451,7 +451,8 @@ hipError_t launch_tgw(const Cgemm3Args& a, hipStream_t st) {
     const int grid = ntiles < cu_count() ? ntiles : cu_count();
     (void)hipGetLastError();
     // B operand reads three fragments ahead of their MFMAs (measured: two ahead 0.355 ms, three 0.352 ms)
-    hipLaunchKernelGGL(tgw_kernel<3>, dim3(grid), dim3(512), 0, st, a, ntiles);
+    // next-gcn B reads: two fragments ahead (three measured 0.342 vs 0.340 ms)
+    hipLaunchKernelGGL((tgw_kernel<3, 2>), dim3(grid), dim3(512), 0, st, a, ntiles);
     return hipGetLastError();
 }
 

@@ -362,9 +362,11 @@ struct Layer {
             }
             // debug hook: per-phase workgroup timing (G, y store, mix, T, epilogue), printed to stderr
             const int F = 14;
-            const int nwg = (N * tin + F - 1) / F;
+            const int ntl = (N * tin + F - 1) / F;
+            const int nwg = 1024;   // >= the persistent grid; unused entries stay zero
             unsigned long long* d = nullptr;
             HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
+            HIP_TRY(hipMemset(d, 0, (size_t)nwg * 6 * 8));
             b.trace = d;
             HIP_TRY(tik::launch_stblock(b, cin, cout, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -372,14 +374,11 @@ struct Layer {
             HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
             HIP_TRY(hipFree(d));
             double ph[5] = {0, 0, 0, 0, 0};
-            unsigned long long lo = ~0ull, hi = 0;
-            for (int w = 0; w < nwg; ++w) {
+            for (int w = 0; w < nwg; ++w)
                 for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
-                lo = std::min(lo, h[6 * w]); hi = std::max(hi, h[6 * w + 5]);
-            }
-            fprintf(stderr, "stblock L%d (%d wg): per-wg us G %.2f wt-issue %.2f mix %.2f T %.2f epi %.2f | span %.1f us\n",
-                    index, nwg, ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100,
-                    ph[4] / nwg / 100, (hi - lo) / 100.0);
+            fprintf(stderr, "stblock L%d (%d tiles): per-tile us G %.2f wt-issue %.2f mix %.2f T %.2f epi %.2f\n",
+                    index, ntl, ph[0] / ntl / 100, ph[1] / ntl / 100, ph[2] / ntl / 100, ph[3] / ntl / 100,
+                    ph[4] / ntl / 100);
             return TIK_OK;
         }
         if (xraw && fuse && stride == 1 && res == RES_CONV && V == 17 && cout == 64 && wr0.p) {
@@ -394,10 +393,12 @@ struct Layer {
                         4.0 * (px_in * cin + px_out * cout + (double)TK * cout * cout), st);
             p.out(out, (size_t)rout * ldz * 2);
             static const bool trace0 = getenv("TIK_STB_TRACE") != nullptr;   // debug: per-phase workgroup timing
-            const int nwg = (N * tin + 13) / 14;
+            const int ntl = (N * tin + 13) / 14;
+            const int nwg = 1024;   // >= the persistent grid
             unsigned long long* d = nullptr;
             if (trace0) {
                 HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
+                HIP_TRY(hipMemset(d, 0, (size_t)nwg * 6 * 8));
                 b.trace = d;
             }
             HIP_TRY(tik::launch_stblock0(b, cout, st));
@@ -409,8 +410,8 @@ struct Layer {
                 double ph[5] = {0, 0, 0, 0, 0};
                 for (int w = 0; w < nwg; ++w)
                     for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
-                fprintf(stderr, "stblock0 L0 (%d wg): per-wg us G(raw) %.2f - %.2f wt-issue %.2f T %.2f epi %.2f\n", nwg,
-                        ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100, ph[4] / nwg / 100);
+                fprintf(stderr, "stblock0 L0 (%d tiles): per-tile us G(raw) %.2f - %.2f wt-issue %.2f T %.2f epi %.2f\n", ntl,
+                        ph[0] / ntl / 100, ph[1] / ntl / 100, ph[2] / ntl / 100, ph[3] / ntl / 100, ph[4] / ntl / 100);
             }
             return TIK_OK;
         }

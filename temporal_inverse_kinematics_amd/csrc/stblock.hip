@@ -23,6 +23,7 @@
 //      split-block stores.
 // HBM traffic per block: read x (+2 halo frames per 14, L2 hits for the
 // neighbour tiles), re-read x for the residual (L2-hot), write out.
+#include <cstdlib>
 #include <type_traits>
 
 #include "cgemm3_dev.h"
@@ -57,7 +58,7 @@ struct StbGeo {
 // block reads 12 B and writes 256 B per pixel, against the 256 + 768 B of
 // the gcn0 + temporal-conv pair.
 template <int CIN, int COUT, int FIN, bool RAW = false>
-__global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
+__global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     using G = StbGeo<CIN, COUT, FIN>;
     constexpr int V = 17;
     constexpr int XSB = RAW ? FIN * V * 4 * 4 : 0;   // data_bn'd keypoints, 4 floats per pixel
@@ -72,18 +73,17 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     const int g = lane >> 4;
     const int QO = a.nwin * a.T;   // frames (flat, input = output for stride 1)
     const int M = QO * V;          // rows
-    int tile;
-    {   // XCD-aware tile order (cgemm3.hip): a contiguous run of tiles per XCD, so
-        // the halo frames a tile shares with its neighbours are L2 hits
+    // persistent: one workgroup per CU walks a contiguous run of tiles (runs
+    // ordered per XCD, so the halo frames neighbouring tiles share are L2 hits)
+    int t_begin, t_end;
+    {
         const int nwg = gridDim.x, bid = blockIdx.x;
         const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
-        tile = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        const int s = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        t_begin = (int)((long long)s * ntiles / nwg);
+        t_end = (int)((long long)(s + 1) * ntiles / nwg);
     }
-    unsigned long long tr[6];
-    if (a.trace) tr[0] = __builtin_amdgcn_s_memrealtime();
-    const int q0 = tile * G::F;   // first output frame
-    const int r0 = q0 * V;        // first output row
-    const int fi0 = q0 - 1;       // first input frame of the z image
+    unsigned long long trs[5] = {0, 0, 0, 0, 0};   // debug: phase sums over this workgroup's tiles
 
     // The mix matrix goes to registers before any DMA is issued (an LDS read
     // after an LDS-DMA gets a compiler vmcnt(0): possible alias):
@@ -97,14 +97,17 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     constexpr int NXI = G::PXR / 8, NXJ = (NXI + 7) / 8;   // x instructions per chunk / per wave (max)
     constexpr int NWJ = COUT / 64;                          // Wg / Wt instructions per wave per chunk
     unsigned xoff[NXJ];
+    auto set_xoff = [&](int tl) {   // x rows of tile tl (input frames tl*F-1 .. tl*F+F)
+        const int f0 = tl * G::F - 1;
 #pragma unroll
-    for (int j = 0; j < NXJ; ++j) {
-        const int idx = wave + 8 * j;
-        const int rr = idx * 8 + (lane >> 3);   // image row: joint rr / 16, frame rr % 16
-        const int ck = (lane & 7) ^ sbf(rr);
-        const long long gr = (long long)(fi0 + (rr & 15)) * V + (rr >> 4);
-        xoff[j] = (idx < NXI && fi0 + (rr & 15) >= 0 && gr < M) ? (unsigned)((gr * a.ldx + 8 * ck) * 2) : DMA_OOB;
-    }
+        for (int j = 0; j < NXJ; ++j) {
+            const int idx = wave + 8 * j;
+            const int rr = idx * 8 + (lane >> 3);   // image row: joint rr / 16, frame rr % 16
+            const int ck = (lane & 7) ^ sbf(rr);
+            const long long gr = (long long)(f0 + (rr & 15)) * V + (rr >> 4);
+            xoff[j] = (idx < NXI && f0 + (rr & 15) >= 0 && gr < M) ? (unsigned)((gr * a.ldx + 8 * ck) * 2) : DMA_OOB;
+        }
+    };
     const int nxj = (NXI - wave + 7) / 8;   // x instructions of this wave
     unsigned wgoff[NWJ], wtoff[NWJ];
 #pragma unroll
@@ -133,6 +136,48 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     };
 
     float* const xsf = reinterpret_cast<float*>(smem + G::SMEM);
+    // the first tile's x image (and Wg); later tiles' are prefetched during the
+    // previous tile's epilogue
+    if (!RAW && t_begin < t_end) {
+        set_xoff(t_begin);
+        issue_g(0, 0);
+        if (G::NKG > 1) issue_g(1, 1);
+    }
+    for (int tile = t_begin; tile < t_end; ++tile) {
+    // re-materialised every tile: hoisted out of the tile loop, the mix's v_readlane
+    // values and the lane-derived addresses would stay live across it and spill
+#pragma unroll
+    for (int k = 0; k < NAM; ++k) asm volatile("" : "+v"(amv[k]));
+    int lt_ = lane;
+    asm volatile("" : "+v"(lt_));
+    const int lane = lt_, g = lt_ >> 4;
+    unsigned long long tr[6];
+    if (a.trace) tr[0] = __builtin_amdgcn_s_memrealtime();
+    const int q0 = tile * G::F;   // first output frame
+    const int r0 = q0 * V;        // first output row
+    const int fi0 = q0 - 1;       // first input frame of the z image
+    // epilogue operands from global memory: the identity residual x of this tile's
+    // rows (raw split halves: hi dwords 0-1, lo 2-3) and the bias. Non-RAW: loaded
+    // right before the first Wt DMAs, so that no wait in the epilogue queues behind
+    // the next tile's x prefetch
+    constexpr int C4 = COUT / 4, RS = 512 / C4, KI = (G::TR + RS - 1) / RS;
+    const int c4 = tid % C4, lr0 = tid / C4, col = 4 * c4;
+    f32x4 rr[KI];
+    f32x4 bv;
+    auto epi_loads = [&]() {
+#pragma unroll
+        for (int k = 0; k < KI; ++k) {
+            rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int lr = lr0 + k * RS;
+            if (!RAW && a.resid && lr < G::TR && r0 + lr < M) {
+                const unsigned short* rp = a.x + (size_t)(r0 + lr) * a.ldx + sbc(col);
+                const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
+                const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
+                rr[k] = f32x4{h[0], h[1], l[0], l[1]};
+            }
+        }
+        bv = *reinterpret_cast<const f32x4*>(a.bias + col);
+    };
     if constexpr (RAW) {
         // ================= 1'. G from the raw keypoints. Thread (frame f, channels
         // co..co+3) of a joint half: waves 0-3 joints 0-8, waves 4-7 joints 9-16; every
@@ -217,8 +262,6 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
     #pragma unroll
         for (int j = 0; j < V; ++j) accg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-        issue_g(0, 0);
-        if (G::NKG > 1) issue_g(1, 1);
     #pragma unroll
         for (int kb = 0; kb < G::NKG; ++kb) {
             if (kb + 1 < G::NKG) {   // chunk kb+1 may stay in flight
@@ -260,6 +303,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (a.trace) tr[1] = __builtin_amdgcn_s_memrealtime();
+        epi_loads();
         // the ring is free: the first Wt chunks load during the mix
     #pragma unroll
         for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
@@ -367,28 +411,20 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
 
     if (a.trace) tr[4] = __builtin_amdgcn_s_memrealtime();
     // ================= 4. epilogue: + bias + x, ReLU, split-block stores
-    constexpr int C4 = COUT / 4, RS = 512 / C4, KI = (G::TR + RS - 1) / RS;
-    const int c4 = tid % C4, lr0 = tid / C4, col = 4 * c4;
-    f32x4 rr[KI];   // raw residual halves (hi dwords 0-1, lo 2-3), loaded before the staging
     float rw[4][4];  // RAW: residual conv weights of this thread's 4 channels
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < 4; ++c) rw[e][c] = (RAW && c < a.c0) ? a.rw[(col + e) * a.c0 + c] : 0.f;
-#pragma unroll
-    for (int k = 0; k < KI; ++k) {
-        rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int lr = lr0 + k * RS;
-        if (!RAW && a.resid && lr < G::TR && r0 + lr < M) {
-            const unsigned short* rp = a.x + (size_t)(r0 + lr) * a.ldx + sbc(col);
-            const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
-            const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
-            rr[k] = f32x4{h[0], h[1], l[0], l[1]};
-        }
-    }
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + col);
+    if (RAW) epi_loads();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // every wave is done reading z: the C tile goes over it
+    // ... and done with the ring: the next tile's x image (and Wg) streams in behind this epilogue
+    if (!RAW && tile + 1 < t_end) {
+        set_xoff(tile + 1);
+        issue_g(0, 0);
+        if (G::NKG > 1) issue_g(1, 1);
+    }
     float* Cs = reinterpret_cast<float*>(zimg);
 #pragma unroll
     for (int i = 0; i < NRB; ++i) {
@@ -430,16 +466,34 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a) {
         *reinterpret_cast<f16x4*>(o + 32) = ol;
     }
     if (a.trace) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
         tr[5] = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0)
-            for (int k = 0; k < 6; ++k) a.trace[6 * blockIdx.x + k] = tr[k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) trs[k] += tr[k + 1] - tr[k];
+    }
+    }   // tile loop
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.trace && tid == 0) {   // cumulative phase sums: trace[6 w + k+1] - trace[6 w + k] = phase k
+        unsigned long long c = 0;
+        a.trace[6 * blockIdx.x] = 0;
+        for (int k = 0; k < 5; ++k) {
+            c += trs[k];
+            a.trace[6 * blockIdx.x + k + 1] = c;
+        }
     }
     TIK_FENCE_END();
 }
 
 bool stblock_ok(int cin, int cout) { return cin == 64 && cout == 64; }
+
+// persistent grid: one workgroup per CU (156 KB of LDS), at most one per tile
+static int stb_grid(int ntiles) {
+    static const bool one_tile = getenv("TIK_STB_ONE_TILE") != nullptr;   // tuning hook: a workgroup per tile
+    if (one_tile) return ntiles;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    return ntiles < cus ? ntiles : cus;
+}
 
 hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st) {
     if (a.nwin <= 0 || a.T <= 0) return hipSuccess;
@@ -452,7 +506,8 @@ hipError_t launch_stblock(const StbArgs& a, int cin, int cout, hipStream_t st) {
     (void)hipGetLastError();
     using G = StbGeo<64, 64, 16>;
     const int QO = a.nwin * a.T;
-    hipLaunchKernelGGL((stblock_kernel<64, 64, 16>), dim3((QO + G::F - 1) / G::F), dim3(512), 0, st, a);
+    const int ntiles = (QO + G::F - 1) / G::F;
+    hipLaunchKernelGGL((stblock_kernel<64, 64, 16>), dim3(stb_grid(ntiles)), dim3(512), 0, st, a, ntiles);
     return hipGetLastError();
 }
 
@@ -468,7 +523,8 @@ hipError_t launch_stblock0(const StbArgs& a, int cout, hipStream_t st) {
     (void)hipGetLastError();
     using G = StbGeo<64, 64, 16>;
     const int QO = a.nwin * a.T;
-    hipLaunchKernelGGL((stblock_kernel<64, 64, 16, true>), dim3((QO + G::F - 1) / G::F), dim3(512), 0, st, b);
+    const int ntiles = (QO + G::F - 1) / G::F;
+    hipLaunchKernelGGL((stblock_kernel<64, 64, 16, true>), dim3(stb_grid(ntiles)), dim3(512), 0, st, b, ntiles);
     return hipGetLastError();
 }
 

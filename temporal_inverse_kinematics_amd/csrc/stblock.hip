@@ -136,6 +136,31 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     };
 
     float* const xsf = reinterpret_cast<float*>(smem + G::SMEM);
+    // RAW: this thread's keypoint elements i = tid + 512 j of a tile's 16 x 17 x 4
+    // image (pixel i/4, channel i%4): data_bn scale / shift are tile-invariant, the
+    // raw values are loaded a tile ahead (kx) during the previous tile's epilogue
+    constexpr int KNE = RAW ? (FIN * V * 4 + 511) / 512 : 1;
+    float kx[KNE], ksc[KNE], ksh[KNE];
+    bool kok[KNE];
+    auto load_kp = [&](int tl) {
+#pragma unroll
+        for (int j = 0; j < KNE; ++j) {
+            const int i = tid + 512 * j, c = i & 3, p = i >> 2;
+            const int v = p % V, fr = tl * G::F - 1 + p / V;
+            kok[j] = RAW && i < FIN * V * 4 && c < a.c0 && fr >= 0 && fr < QO;
+            kx[j] = kok[j] ? a.xraw[((size_t)fr * V + v) * a.c0 + c] : 0.f;
+        }
+    };
+    if constexpr (RAW) {
+#pragma unroll
+        for (int j = 0; j < KNE; ++j) {
+            const int i = tid + 512 * j, c = i & 3, v = (i >> 2) % V;
+            const bool ok = i < FIN * V * 4 && c < a.c0;
+            ksc[j] = ok ? a.bn_sc[v * a.c0 + c] : 0.f;
+            ksh[j] = ok ? a.bn_sh[v * a.c0 + c] : 0.f;
+        }
+        if (t_begin < t_end) load_kp(t_begin);
+    }
     // the first tile's x image (and Wg); later tiles' are prefetched during the
     // previous tile's epilogue
     if (!RAW && t_begin < t_end) {
@@ -144,6 +169,12 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
         if (G::NKG > 1) issue_g(1, 1);
     }
     for (int tile = t_begin; tile < t_end; ++tile) {
+    // every wave is done with the previous tile's epilogue LDS reads (C tile over the
+    // z image, RAW keypoint image) before this tile writes them (zero rows, keypoints)
+    if (tile != t_begin) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
     // re-materialised every tile: hoisted out of the tile loop, the mix's v_readlane
     // values and the lane-derived addresses would stay live across it and spill
 #pragma unroll
@@ -184,22 +215,25 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
         // thread forms y for all 17 joints (the mix input), each half mixes its joints.
         const int f = tid & 15, co = 4 * ((tid >> 4) & 15), half = wave >> 2;
         const int w0 = half ? 9 : 0;
-        // weights and bias2' first: their latency overlaps the keypoint staging
+        // weights and bias2' (L2 hits), re-loaded every tile through opaque pointers:
+        // hoisted out of the tile loop they would stay live across it and spill
+        const float* wg0p = a.wg0;
+        const float* b2p = a.bias2;
+        asm volatile("" : "+s"(wg0p), "+s"(b2p));
         float w[4][4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? a.wg0[(co + e) * a.ldwg0 + c] : 0.f;
+            for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? wg0p[(co + e) * a.ldwg0 + c] : 0.f;
         f32x4 b[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) b[k] = w0 + k < V ? *reinterpret_cast<const f32x4*>(a.bias2 + (w0 + k) * COUT + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-        // data_bn(x) of the 16 frames -> LDS
-        for (int i = tid; i < FIN * V * 4; i += 512) {
-            const int c = i & 3, p = i >> 2;
-            const int v = p % V, fr = fi0 + p / V;
-            float val = 0.f;
-            if (c < a.c0 && fr >= 0 && fr < QO) val = fmaf(a.xraw[((size_t)fr * V + v) * a.c0 + c], a.bn_sc[v * a.c0 + c], a.bn_sh[v * a.c0 + c]);
-            xsf[i] = val;
+        for (int k = 0; k < 9; ++k) b[k] = w0 + k < V ? *reinterpret_cast<const f32x4*>(b2p + (w0 + k) * COUT + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+        // data_bn(x) of the 16 frames -> LDS (the raw keypoints were loaded during the
+        // previous tile's epilogue)
+#pragma unroll
+        for (int j = 0; j < KNE; ++j) {
+            const int i = tid + 512 * j;
+            if (i < FIN * V * 4) xsf[i] = kok[j] ? fmaf(kx[j], ksc[j], ksh[j]) : 0.f;
         }
         if (tid < G::NKB * 8)   // zero rows (taps past a window edge)
             *reinterpret_cast<f32x4*>(zimg + (tid >> 3) * G::ZB + G::ZR * 128 + (tid & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -425,6 +459,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
         issue_g(0, 0);
         if (G::NKG > 1) issue_g(1, 1);
     }
+    if (RAW && tile + 1 < t_end) load_kp(tile + 1);
     float* Cs = reinterpret_cast<float*>(zimg);
 #pragma unroll
     for (int i = 0; i < NRB; ++i) {

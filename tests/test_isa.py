@@ -119,3 +119,20 @@ def test_gpw_loop_memory_instruction_counts(tmp_path):
         assert c == Counter({"buffer_load_dwordx4": ndma, "global_store_dwordx4": nst}), (key, c)
         seen.add(key)
     assert seen == set(want), seen
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src_name", ["stblock.hip", "gpw.hip", "tgw.hip", "fk.hip"])
+def test_counted_wait_kernels_do_not_spill(tmp_path, src_name):
+    """Kernels with counted vmcnt waits (LDS-DMA rings, prefetch across tiles)
+    must not spill: a scratch load or store is a vector-memory instruction and
+    would shift every count after it."""
+    src = os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", src_name)
+    out = tmp_path / "k.s"
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
+                        "--cuda-device-only", "-S", src, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    text = out.read_text()
+    assert not re.search(r"^\s+scratch_", text, re.M), "scratch instructions"
+    spills = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", text)]
+    assert spills and max(spills) == 0, spills

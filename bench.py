@@ -36,7 +36,9 @@ KERNEL_SYMBOLS = {
     "T3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 0>",
     "T3_128x64": "tik::tgemm_kernel<128, 64, 4, 2, 3, 0>",
     "TG3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 7>",
-    "TW_128": "tik::tgw_kernel",
+    "TW_128": "tik::tgw_kernel<3, 2>",
+    "GP_128": "tik::gpw_kernel<64, 128, 4, 4, 1>",
+    "GP_256": "tik::gpw_kernel<128, 256, 3, 8, 2>",
     "TH_128x128": "tik::tconv_halo_kernel<128, 2, 4>",
     "TH_128x64": "tik::tconv_halo_kernel<64, 4, 2>",
     "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",
@@ -58,7 +60,8 @@ def _pmc_traffic(path, label):
     sym = KERNEL_SYMBOLS.get(label)
     kern = json.load(open(path)).get("kernels", {})
     for k, v in kern.items():
-        if sym and k.replace("void ", "").strip() == sym:
+        name = k.replace("void ", "").strip()
+        if sym and (name == sym or ("<" not in sym and name.startswith(sym + "<"))):
             return v["hbm_bytes_per_dispatch"], os.path.relpath(path, REPO)
     return None, os.path.relpath(path, REPO)
 

@@ -103,3 +103,22 @@ def test_no_oracle_import_in_product():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace('"""', ""), f
+
+
+def test_bench_kernel_symbols_match_pmc_profile():
+    """bench.py's roofline `traffic` looks the dominant kernel up by symbol in the
+    newest committed PMC summary; every kernel of the default path must resolve
+    (a templated kernel renamed in the profiler output made it silently null)."""
+    import glob
+    import importlib.util
+    import json
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    newest = sorted(glob.glob(os.path.join(repo, "profiles", "*pmc_traffic*.json")), key=os.path.getmtime)[-1]
+    kernels = json.load(open(newest))["kernels"]
+    for label in ("TW_128", "GP_128", "GP_256", "TG3_128x128", "T3_128x128", "B3_64", "B0_64", "G3_272x128", "H3_64x64"):
+        traffic, src = bench._pmc_traffic(newest, label)
+        assert traffic is not None and traffic > 0, (label, bench.KERNEL_SYMBOLS.get(label), list(kernels))

@@ -49,7 +49,7 @@ struct StbGeo {
     static_assert(COUT == 64, "G: one 16-channel block per wave for waves 0-3");
     static_assert(CT <= ZBYTES, "C tile must fit over the z image");
     static_assert(SMEM <= 163840, "LDS");
-    static_assert(TSLOTS >= 2, "T ring");
+    static_assert(TSLOTS == NKT, "T: the whole Wt resident in the ring (no per-chunk waits)");
 };
 
 // RAW: the first block straight from the raw keypoints (layer0.hip's gcn0
@@ -61,7 +61,8 @@ template <int CIN, int COUT, int FIN, bool RAW = false>
 __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     using G = StbGeo<CIN, COUT, FIN>;
     constexpr int V = 17;
-    constexpr int XSB = RAW ? FIN * V * 4 * 4 : 0;   // data_bn'd keypoints, 4 floats per pixel
+    // RAW: data_bn'd keypoints, 4 floats per pixel; otherwise bias2 [17][COUT] (the same 4,352 B)
+    constexpr int XSB = RAW ? FIN * V * 4 * 4 : V * COUT * 4;
     static_assert(G::SMEM + XSB <= 163840, "LDS");
     __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM + XSB];   // the only LDS object
     unsigned char* const zimg = smem;
@@ -160,14 +161,29 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
             ksh[j] = ok ? a.bn_sh[v * a.c0 + c] : 0.f;
         }
         if (t_begin < t_end) load_kp(t_begin);
+        // RAW never uses the ring for anything else: the whole Wt stays resident
+        // for every tile of the run (the first T's wait covers it)
+#pragma unroll
+        for (int c = 0; c < G::NKT; ++c) issue_t(c, c);
     }
     // the first tile's x image (and Wg); later tiles' are prefetched during the
     // previous tile's epilogue
+    // non-RAW: bias2 in LDS for the whole run, written before any DMA is in flight
+    // (an LDS access behind an LDS-DMA gets a compiler vmcnt(0): possible alias)
+    float* const b2s = reinterpret_cast<float*>(smem + G::SMEM);
+    if constexpr (!RAW) {
+        for (int i = tid; i < V * COUT; i += 512) b2s[i] = a.bias2[i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (!RAW && t_begin < t_end) {
         set_xoff(t_begin);
         issue_g(0, 0);
         if (G::NKG > 1) issue_g(1, 1);
     }
+    // this thread's epilogue bias (4 channels): non-RAW keeps it for the whole
+    // run (a load inside the tile would queue behind the x prefetch), RAW
+    // (no registers to spare) loads it in each epilogue
+    const f32x4 bv_run = RAW ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(a.bias + 4 * (tid % (COUT / 4)));
     for (int tile = t_begin; tile < t_end; ++tile) {
     // every wave is done with the previous tile's epilogue LDS reads (C tile over the
     // z image, RAW keypoint image) before this tile writes them (zero rows, keypoints)
@@ -187,27 +203,25 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     const int q0 = tile * G::F;   // first output frame
     const int r0 = q0 * V;        // first output row
     const int fi0 = q0 - 1;       // first input frame of the z image
-    // epilogue operands from global memory: the identity residual x of this tile's
-    // rows (raw split halves: hi dwords 0-1, lo 2-3) and the bias. Non-RAW: loaded
-    // right before the first Wt DMAs, so that no wait in the epilogue queues behind
-    // the next tile's x prefetch
+    // epilogue operands: the identity residual x of this tile's rows (raw split
+    // halves: hi dwords 0-1, lo 2-3), read from the LDS x image at the end of G
+    // (it holds exactly these rows: output frame q0 + t is image frame t + 1), and
+    // the bias
     constexpr int C4 = COUT / 4, RS = 512 / C4, KI = (G::TR + RS - 1) / RS;
     const int c4 = tid % C4, lr0 = tid / C4, col = 4 * c4;
     f32x4 rr[KI];
-    f32x4 bv;
-    auto epi_loads = [&]() {
+    auto resid_from_image = [&]() {
+        const unsigned char* X = ring + (col >> 5) * G::GSLOT;
+        const int cc = col & 31, u = cc >> 3, bo = (cc & 7) * 2;
 #pragma unroll
         for (int k = 0; k < KI; ++k) {
-            rr[k] = f32x4{0.f, 0.f, 0.f, 0.f};
             const int lr = lr0 + k * RS;
-            if (!RAW && a.resid && lr < G::TR && r0 + lr < M) {
-                const unsigned short* rp = a.x + (size_t)(r0 + lr) * a.ldx + sbc(col);
-                const f32x2 h = *reinterpret_cast<const f32x2*>(rp);
-                const f32x2 l = *reinterpret_cast<const f32x2*>(rp + 32);
-                rr[k] = f32x4{h[0], h[1], l[0], l[1]};
-            }
+            const int tl = lr / V, v = lr - tl * V, ir = 16 * v + tl + 1;
+            const bool ok = a.resid && lr < G::TR && r0 + lr < M;
+            const f32x2 h = *reinterpret_cast<const f32x2*>(X + sbo(ok ? ir : 0, u) + bo);
+            const f32x2 l = *reinterpret_cast<const f32x2*>(X + sbo(ok ? ir : 0, 4 + u) + bo);
+            rr[k] = ok ? f32x4{h[0], h[1], l[0], l[1]} : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        bv = *reinterpret_cast<const f32x4*>(a.bias + col);
     };
     if constexpr (RAW) {
         // ================= 1'. G from the raw keypoints. Thread (frame f, channels
@@ -283,11 +297,10 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
             }
         }
         if (a.trace) tr[1] = tr[2] = __builtin_amdgcn_s_memrealtime();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // the resident Wt landed (only the first tile waits on it; the previous
+        // epilogue's stores are long done) and the z image is complete
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        // the ring is free: the first Wt chunks (the T loop's first wait covers them)
-#pragma unroll
-        for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
         if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
     } else {
         // ================= 1. G: y^T = Wg'^T x^T; waves 0-3 own channel block `wave`, all 17 joints
@@ -327,20 +340,20 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
                 issue_g(kb + 2, kb & 1);
             }
         }
-        // bias2 of this lane's 4 channels for all joints: loaded before the Wt
-        // DMAs below so its wait does not queue behind them
+        // bias2 of this lane's 4 channels for all joints, from LDS before the Wt
+        // DMAs below (no DMA in flight: no alias wait)
         const int mc = wave * 16 + 4 * g;   // mix channels mc .. mc+3 (waves 0-3)
         f32x4 b2r[V];
     #pragma unroll
         for (int w = 0; w < V; ++w)
-            b2r[w] = gw ? *reinterpret_cast<const f32x4*>(a.bias2 + w * COUT + mc) : f32x4{0.f, 0.f, 0.f, 0.f};
+            b2r[w] = gw ? *reinterpret_cast<const f32x4*>(b2s + w * COUT + mc) : f32x4{0.f, 0.f, 0.f, 0.f};
+        resid_from_image();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (a.trace) tr[1] = __builtin_amdgcn_s_memrealtime();
-        epi_loads();
-        // the ring is free: the first Wt chunks load during the mix
+        // the ring is free: the whole Wt loads during the mix
     #pragma unroll
-        for (int c = 0; c < G::TSLOTS - 1; ++c) issue_t(c, c);
+        for (int c = 0; c < G::NKT; ++c) issue_t(c, c);
         if (a.trace) tr[2] = __builtin_amdgcn_s_memrealtime();
 
         // ================= 2. mix in registers: z[w] = ReLU(bias2[w] + sum_v A[v][w] y[v])
@@ -375,7 +388,8 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
             const int i = tid - 256;
             *reinterpret_cast<f32x4*>(zimg + (i >> 3) * G::ZB + G::ZR * 128 + (i & 7) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // the whole Wt landed and the z image is complete
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (a.trace) tr[3] = __builtin_amdgcn_s_memrealtime();
     }
@@ -409,17 +423,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
 #pragma unroll
     for (int c = 0; c < G::NKT; ++c) {
         const int tap = c / G::NKB, kb = c % G::NKB;
-        // chunk c retired; chunks c+1 .. c+TSLOTS-2 may stay in flight
-        const int younger = (G::TSLOTS - 2 < G::NKT - 1 - c) ? G::TSLOTS - 2 : G::NKT - 1 - c;
-        if (younger >= 4) wait_vm<4 * NWJ>();
-        else if (younger == 3) wait_vm<3 * NWJ>();
-        else if (younger == 2) wait_vm<2 * NWJ>();
-        else if (younger == 1) wait_vm<NWJ>();
-        else wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (c + G::TSLOTS - 1 < G::NKT) issue_t(c + G::TSLOTS - 1, (c + G::TSLOTS - 1) % G::TSLOTS);
-        const unsigned char* B = ring + (c % G::TSLOTS) * G::WS;
+        const unsigned char* B = ring + c * G::WS;
         const unsigned char* A = zimg + kb * G::ZB;
         f16x8 bh[4], bl[4];
 #pragma unroll
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < 4; ++c) rw[e][c] = (RAW && c < a.c0) ? a.rw[(col + e) * a.c0 + c] : 0.f;
-    if (RAW) epi_loads();
+    const f32x4 bv = RAW ? *reinterpret_cast<const f32x4*>(a.bias + col) : bv_run;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // every wave is done reading z: the C tile goes over it
     // ... and done with the ring: the next tile's x image (and Wg) streams in behind this epilogue

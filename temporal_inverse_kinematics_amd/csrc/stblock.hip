@@ -63,8 +63,9 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     constexpr int V = 17;
     // RAW: data_bn'd keypoints, 4 floats per pixel; otherwise bias2 [17][COUT] (the same 4,352 B)
     constexpr int XSB = RAW ? FIN * V * 4 * 4 : V * COUT * 4;
-    static_assert(G::SMEM + XSB <= 163840, "LDS");
-    __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM + XSB];   // the only LDS object
+    constexpr int BSB = RAW ? COUT * 4 : 0;   // RAW: the epilogue bias in LDS
+    static_assert(G::SMEM + XSB + BSB <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM + XSB + BSB];   // the only LDS object
     unsigned char* const zimg = smem;
     unsigned char* const ring = smem + G::ZBYTES;
 
@@ -144,9 +145,11 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     float kx[KNE], ksc[KNE], ksh[KNE];
     bool kok[KNE];
     auto load_kp = [&](int tl) {
+        int t_ = tid;   // opaque: the per-element joint / frame offsets are not hoisted out of the tile loop
+        asm volatile("" : "+v"(t_));
 #pragma unroll
         for (int j = 0; j < KNE; ++j) {
-            const int i = tid + 512 * j, c = i & 3, p = i >> 2;
+            const int i = t_ + 512 * j, c = i & 3, p = i >> 2;
             const int v = p % V, fr = tl * G::F - 1 + p / V;
             kok[j] = RAW && i < FIN * V * 4 && c < a.c0 && fr >= 0 && fr < QO;
             kx[j] = kok[j] ? a.xraw[((size_t)fr * V + v) * a.c0 + c] : 0.f;
@@ -161,6 +164,9 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
             ksh[j] = ok ? a.bn_sh[v * a.c0 + c] : 0.f;
         }
         if (t_begin < t_end) load_kp(t_begin);
+        float* bsl = reinterpret_cast<float*>(smem + G::SMEM + XSB);
+        if (tid < COUT) bsl[tid] = a.bias[tid];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // written before the first DMA
         // RAW never uses the ring for anything else: the whole Wt stays resident
         // for every tile of the run (the first T's wait covers it)
 #pragma unroll
@@ -324,14 +330,28 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
                 const int r = wave * 16 + (lane & 15);
                 const f16x8 ah = *reinterpret_cast<const f16x8*>(W + sbo(r, g));
                 const f16x8 al = *reinterpret_cast<const f16x8*>(W + sbo(r, 4 + g));
+                // B fragments read GPD joints ahead of their MFMAs (read right before
+                // use, every fragment exposed the LDS latency)
+                constexpr int GPD = 3;
+                f16x8 pbh[GPD + 1], pbl[GPD + 1];
+                auto ldb = [&](int j) {
+                    const int rx = j * 16 + (lane & 15);
+                    pbh[j % (GPD + 1)] = *reinterpret_cast<const f16x8*>(X + sbo(rx, g));
+                    pbl[j % (GPD + 1)] = *reinterpret_cast<const f16x8*>(X + sbo(rx, 4 + g));
+                };
+    #pragma unroll
+                for (int j = 0; j < GPD; ++j) ldb(j);
     #pragma unroll
                 for (int j = 0; j < V; ++j) {
-                    const int rx = j * 16 + (lane & 15);
-                    const f16x8 bh = *reinterpret_cast<const f16x8*>(X + sbo(rx, g));
-                    const f16x8 bl = *reinterpret_cast<const f16x8*>(X + sbo(rx, 4 + g));
+                    if (j + GPD < V) ldb(j + GPD);
+                    // fence the scheduler: under this kernel's register pressure it
+                    // otherwise sinks every read to right before its MFMA
+                    __builtin_amdgcn_sched_barrier(0);
+                    const f16x8 bh = pbh[j % (GPD + 1)], bl = pbl[j % (GPD + 1)];
                     accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, accg[j], 0, 0, 0);
                     accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, accg[j], 0, 0, 0);
                     accg[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, accg[j], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
             if (kb + 2 < G::NKG) {
@@ -454,7 +474,6 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < 4; ++c) rw[e][c] = (RAW && c < a.c0) ? a.rw[(col + e) * a.c0 + c] : 0.f;
-    const f32x4 bv = RAW ? *reinterpret_cast<const f32x4*>(a.bias + col) : bv_run;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // every wave is done reading z: the C tile goes over it
     // ... and done with the ring: the next tile's x image (and Wg) streams in behind this epilogue
@@ -477,6 +496,7 @@ __global__ __launch_bounds__(512) void stblock_kernel(StbArgs a, int ntiles) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // LDS only: the residual loads stay in flight
+    const f32x4 bv = RAW ? *reinterpret_cast<const f32x4*>(smem + G::SMEM + XSB + 4 * col) : bv_run;
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
         const int lr = lr0 + k * RS, row = r0 + lr;

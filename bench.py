@@ -48,12 +48,12 @@ KERNEL_SYMBOLS = {
 }
 
 
-def _pmc_traffic(path, label):
-    """HBM bytes per dispatch of the kernel behind `label` from a PMC summary
-    (scripts/pmc_traffic.py output), or None."""
+def _pmc_value(path, label, pattern, field):
+    """`field` of the kernel behind `label` in a PMC summary (scripts/pmc_traffic.py
+    or pmc_mfma.py output; default: the newest profiles/`pattern`), or None."""
     import glob
     if path is None:
-        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")), key=os.path.getmtime)
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), key=os.path.getmtime)
         path = cands[-1] if cands else None
     if not path or not os.path.exists(path):
         return None, None
@@ -62,8 +62,18 @@ def _pmc_traffic(path, label):
     for k, v in kern.items():
         name = k.replace("void ", "").strip()
         if sym and (name == sym or ("<" not in sym and name.startswith(sym + "<"))):
-            return v["hbm_bytes_per_dispatch"], os.path.relpath(path, REPO)
+            return v.get(field), os.path.relpath(path, REPO)
     return None, os.path.relpath(path, REPO)
+
+
+def _pmc_traffic(path, label):
+    """HBM bytes per dispatch of the kernel behind `label` (scripts/pmc_traffic.py)."""
+    return _pmc_value(path, label, "*pmc_traffic*.json", "hbm_bytes_per_dispatch")
+
+
+def _pmc_mfma(path, label):
+    """MFMA-busy fraction of the kernel behind `label` (scripts/pmc_mfma.py)."""
+    return _pmc_value(path, label, "*pmc_mfma*.json", "mfma_busy_frac")
 
 
 def _cpu_baseline(T: int, seconds: float = 12.0):
@@ -104,6 +114,8 @@ def main():
                     help="diagnostic: no per-launch HIP events in the timed region (no roofline)")
     ap.add_argument("--pmc-traffic", default=None,
                     help="PMC traffic summary (scripts/pmc_traffic.py); default: newest profiles/*pmc_traffic*.json")
+    ap.add_argument("--pmc-mfma", default=None,
+                    help="PMC MFMA-busy summary (scripts/pmc_mfma.py); default: newest profiles/*pmc_mfma*.json")
     args = ap.parse_args()
 
     import numpy as np
@@ -245,6 +257,7 @@ def main():
         else:
             bound, achieved, peak, unit = "mfma", tflops, mpeak, "TFLOP/s"
         traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom)
+        mfma_busy, mfma_src = _pmc_mfma(args.pmc_mfma, dom)
         kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
                        "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 2), "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1)}
                    for k, v in agg.items()}
@@ -272,6 +285,10 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
+                         "mfma_busy": None if mfma_busy is None else round(mfma_busy, 4),
+                         "mfma_busy_basis": "PMC SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), "
+                                            "single-stream dispatches (scripts/pmc_mfma.py)",
+                         "mfma_busy_source": mfma_src,
                          "algorithmic_bytes_per_launch": round(tot_by / cnt),
                          "algorithmic_flops_per_launch": round(tot_fl / cnt),
                          "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,

@@ -16,18 +16,11 @@ tail -3 $OUT/pytest_gpu_$TAG.log; echo "pytest rc=$rc"; ok $rc || exit $rc
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1; rc=$?
 tail -2 $OUT/smoke_$TAG.log; echo "smoke rc=$rc"; [ $rc -eq 0 ] || exit $rc
-echo "== pmc passes"
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $OUT/pmc_fetch_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-compare > /dev/null 2> $OUT/pmc_fetch_$TAG.err; rc=$?
-echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $OUT/pmc_write_$TAG -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-compare > /dev/null 2> $OUT/pmc_write_$TAG.err; rc=$?
-echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-python scripts/pmc_traffic.py $OUT/pmc_fetch_$TAG $OUT/pmc_write_$TAG $OUT/pmc_traffic_$TAG.json > $OUT/pmc_traffic_$TAG.txt 2>&1
-cat $OUT/pmc_traffic_$TAG.txt
-echo "== rocprofv3 kernel stats"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-compare > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err; rc=$?
-echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+echo "== pmc passes + kernel stats (single-stream)"
+bash scripts/gpu_pmc_all.sh $TAG; rc=$?
+echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo "== bench"
-timeout -k 10 400 python bench.py --pmc-traffic $OUT/pmc_traffic_$TAG.json > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err; rc=$?
+timeout -k 10 400 python bench.py --pmc-traffic $OUT/pmc_traffic_$TAG.json --pmc-mfma $OUT/pmc_mfma_$TAG.json > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err; rc=$?
 tail -c 1500 $OUT/bench_$TAG.json; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo "== stream"
 timeout -k 10 300 python bench_stream.py --frames 3000 > $OUT/stream_$TAG.json 2> $OUT/stream_$TAG.err; rc=$?

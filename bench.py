@@ -48,13 +48,24 @@ KERNEL_SYMBOLS = {
 }
 
 
+def newest_profile(pattern):
+    """The newest profiles/`pattern` by the rNN_vMM tag in its name (file
+    mtimes are checkout times, not measurement order), or None."""
+    import glob
+    import re
+
+    def key(p):
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(p))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), key=key)
+    return cands[-1] if cands else None
+
+
 def _pmc_value(path, label, pattern, field):
     """`field` of the kernel behind `label` in a PMC summary (scripts/pmc_traffic.py
     or pmc_mfma.py output; default: the newest profiles/`pattern`), or None."""
-    import glob
     if path is None:
-        cands = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), key=os.path.getmtime)
-        path = cands[-1] if cands else None
+        path = newest_profile(pattern)
     if not path or not os.path.exists(path):
         return None, None
     sym = KERNEL_SYMBOLS.get(label)

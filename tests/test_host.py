@@ -117,7 +117,9 @@ def test_bench_kernel_symbols_match_pmc_profile():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    newest = sorted(glob.glob(os.path.join(repo, "profiles", "*pmc_traffic*.json")), key=os.path.getmtime)[-1]
+    newest = bench.newest_profile("*pmc_traffic*.json")
+    tags = [os.path.basename(p)[:7] for p in glob.glob(os.path.join(repo, "profiles", "r*_v*_pmc_traffic.json"))]
+    assert max(tags, key=lambda s: (int(s[1:3]), int(s.split("_v")[1].rstrip("_")))) in os.path.basename(newest)
     kernels = json.load(open(newest))["kernels"]
     for label in ("TW_128", "GP_128", "GP_256", "TG3_128x128", "T3_128x128", "B3_64", "B0_64", "G3_272x128", "H3_64x64"):
         traffic, src = bench._pmc_traffic(newest, label)

@@ -187,6 +187,42 @@ int tik_train_windows(const float* joints, int n_joints, const float* poses, int
                       float* windows, float* target, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Training step (optimizer half). Replaces
+ * IKPoseTrainer.training_step (pose_trainer.py:146-155) as Lightning runs it:
+ * train-mode forward (batch-statistics BatchNorm with the running-stat
+ * update, Dropout(0.7) in the head, pose_trainer.py:89-92), nn.MSELoss
+ * against the target poses (PoseLosses, :42-50), backward, and one
+ * torch.optim.Adam(lr) update (configure_optimizers, :196-197).
+ *
+ * tik_trainer_create: the PoseRegressor state dict (as tik_model_create,
+ *   incl. "tik.strides"); parameters and buffers are copied to the device.
+ * tik_trainer_step: x [N][T][17][3], target [N][T'][66] (device fp32);
+ *   dropout_mask [N*T'][512] of 0/1 (device), or NULL = a counter-based mask
+ *   keyed by `seed`; loss: device float (or NULL). Stream-ordered.
+ * tik_trainer_count / _tensor / _read: the state dict after the last step,
+ *   in the reference's names and layouts (kind 0 = parameter, 1 = buffer);
+ *   what = 0 value, 1 last gradient, 2 Adam exp_avg, 3 Adam exp_avg_sq,
+ *   copied to a device pointer. tik_trainer_steps: updates taken
+ *   (BatchNorm num_batches_tracked).
+ * ---------------------------------------------------------------------- */
+typedef struct tik_trainer* tik_trainer_t;
+int tik_trainer_create(const tik_tensor* tensors, int n_tensors, float lr, tik_trainer_t* out);
+int tik_trainer_destroy(tik_trainer_t t);
+int tik_trainer_step(tik_trainer_t t, const float* x, int N, int T, const float* target, const float* dropout_mask,
+                     unsigned long long seed, float* loss, void* stream);
+int tik_trainer_out_frames(tik_trainer_t t, int T);
+int tik_trainer_count(tik_trainer_t t);
+int tik_trainer_tensor(tik_trainer_t t, int i, char* name, int name_len, int64_t* shape4, int* ndim, int* kind);
+int tik_trainer_read(tik_trainer_t t, int i, int what, float* dst, void* stream);
+long long tik_trainer_steps(tik_trainer_t t);
+/* Debug / test hook: the last step's saved activations of block `layer`
+ * (which 0 output, 2 tcn conv output, 3 post-ReLU tcn input, 4 graph-mix
+ * output, 5 gcn conv output; 6 the head's first Linear output), and with
+ * TIK_TRAIN_DEBUG=1 (TIK_TRAIN_DEBUG_LAYER=l) its input gradient (1) and
+ * backward intermediates (10..14); n floats to device dst. */
+int tik_trainer_debug(tik_trainer_t t, int which, int layer, float* dst, long long n, void* stream);
+
+/* ------------------------------------------------------------------------
  * SMPL-X forward kinematics + linear blend skinning (the FK check).
  * Replaces common/smpl_util.py:8-82 (load_smplx_models / run_smpl_inference)
  * and the third-party smplx.SMPLX.forward it calls (smpl_util.py:67-69;

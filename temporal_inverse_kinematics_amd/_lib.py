@@ -68,6 +68,16 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_fk_num_verts": (_I, (_P,)),
     "tik_fk_reserve": (_I, (_P, _I)),
     "tik_fk_forward": (_I, (_P, _P, _P, _P, _P, _I, _P, _P, _P)),
+    "tik_trainer_create": (_I, (ctypes.POINTER(TikTensor), _I, ctypes.c_float, ctypes.POINTER(_P))),
+    "tik_trainer_destroy": (_I, (_P,)),
+    "tik_trainer_step": (_I, (_P, _P, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P)),
+    "tik_trainer_out_frames": (_I, (_P, _I)),
+    "tik_trainer_count": (_I, (_P,)),
+    "tik_trainer_tensor": (_I, (_P, _I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_I),
+                                ctypes.POINTER(_I))),
+    "tik_trainer_read": (_I, (_P, _I, _I, _P, _P)),
+    "tik_trainer_steps": (ctypes.c_longlong, (_P,)),
+    "tik_trainer_debug": (_I, (_P, _I, _I, _P, ctypes.c_longlong, _P)),
 }
 
 _lib = None

@@ -1,0 +1,217 @@
+"""The training step on the GPU (GpuTrainer -> libtik tik_trainer_step) against
+the CPU oracle (oracle/train.py: the reference's training step restated in
+plain PyTorch fp32 autograd, pinned to tests/golden/train.npz, which the
+reference's own IKPoseTrainer produced: tests/test_oracle.py) on identical
+batches and dropout masks.
+
+ReLU branches. A pre-activation within rounding (~1e-6) of zero may fall on
+either side in two correct fp32 implementations, and one such element changes
+its gradient by up to the gradient's full size; through the BatchNorm
+backward the difference spreads over the channel and every layer below
+(measured on the fixture batch: one element of block 4, 6.7e-7 in the
+reference, -0 here, moved layer 0-4 gradients by 1-20 %). So the backward is
+checked with the oracle taking the GPU step's ReLU / LeakyReLU branches
+(oracle.train.forward(relu_masks=...)), and the forward separately: every
+block output within 2e-5 of the oracle's, which bounds any branch
+disagreement to pre-activations of that size.
+
+Tolerances: loss 1e-5 relative; gradients max|gpu - oracle| <= 1e-4 *
+max|oracle| per tensor (measured ~2e-6), except the biases in front of a
+train-mode BatchNorm (tcn.2.bias, residual.0.bias), whose true gradient is
+exactly zero (the BatchNorm removes any per-channel constant): both sides
+hold rounding noise, checked as |g| <= 1e-5; the Adam change of every element
+whose gradient is at least 1e-3 of its tensor's largest within 2e-3 * lr, and
+of every element within steps * lr; running statistics 1e-5 relative. A second
+step's loss (and the running statistics after it) against the fixture: 1e-3 relative, because Adam's first update
+is lr * g / (|g| + 1e-8) = +-lr for any gradient above ~1e-8, so elements
+whose gradient is rounding noise (those biases, near-zero entries of the
+2.2M-value head weight) move by +-lr with a sign set by summation order, in
+the reference as in any reimplementation (measured 1.0e-4)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import stgcn as orc
+from oracle import train as otr
+
+pytestmark = pytest.mark.gpu
+
+ZERO_GRAD = ("tcn.2.bias", "residual.0.bias")
+STRIDES = [s for _, _, s in otr.IK_LAYERS]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    return True
+
+
+def _model(sd, win):
+    from temporal_inverse_kinematics_amd.models import IKPoseTrainer, default_hparams
+    m = IKPoseTrainer(default_hparams(win_size=win))
+    own = m.regressor.state_dict()
+    m.regressor.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items() if k in own}, strict=False)
+    return m
+
+
+def _weights(seed=0):
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    return syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=seed)
+
+
+def _frames(T):
+    t = [T]
+    for s in STRIDES:
+        t.append((t[-1] - 1) // s + 1)
+    return t
+
+
+def _gpu_masks(tr, N, T):
+    """The GPU step's branch at every ReLU / LeakyReLU, in the oracle's layouts."""
+    tf = _frames(T)
+    m = {}
+    for l, (_, cout, _) in enumerate(otr.IK_LAYERS):
+        H = tr.saved("H", l, (N, tf[l], 17, cout))
+        O = tr.saved("O", l, (N, tf[l + 1], 17, cout))
+        m[("H", l)] = (H > 0).float().permute(0, 3, 1, 2).contiguous().cpu()
+        m[("O", l)] = (O > 0).float().permute(0, 3, 1, 2).contiguous().cpu()
+    m["P"] = (tr.saved("P", 0, (N * tf[-1], 512)) > 0).float().cpu()
+    return m
+
+
+def _check_forward(tr, sd, x, mask):
+    """Every block output of the GPU step against the oracle's natural forward."""
+    N, T = x.shape[:2]
+    P, B = otr.split_state(sd)
+    taps = []
+    with torch.no_grad():
+        otr.forward(P, B, torch.from_numpy(x), torch.from_numpy(mask), taps=taps)
+    tf = _frames(T)
+    for l, h in enumerate(taps):
+        ref = h.permute(0, 2, 3, 1).numpy()
+        got = tr.saved("O", l, (N, tf[l + 1], 17, ref.shape[-1])).cpu().numpy()
+        err = np.abs(got - ref).max()
+        assert err <= 2e-5 * max(1.0, np.abs(ref).max()), (l, err)
+
+
+def _check_step(tr, sd, x, tgt, mask, lr, loss_gpu):
+    """One GPU step against the oracle taking the same branches: loss, every
+    gradient, every updated parameter, the running statistics."""
+    N, T = x.shape[:2]
+    losses, grads_ref, state_ref = otr.train_steps(sd, [(x, tgt, mask)], lr=lr, relu_masks=_gpu_masks(tr, N, T))
+    np.testing.assert_allclose(loss_gpu, losses[0], rtol=1e-5)
+    grads = {k: v.cpu().numpy() for k, v in tr.grads().items()}
+    state = {k: v.cpu().numpy() for k, v in tr.state_dict().items() if not k.endswith("num_batches_tracked")}
+    for k in otr.param_names():
+        g, r = grads[k], grads_ref[k]
+        if k.endswith(ZERO_GRAD):
+            assert np.abs(g).max() <= 1e-5 and np.abs(r).max() <= 1e-5, k
+        else:
+            err = np.abs(g - r).max()
+            assert err <= 1e-4 * np.abs(r).max() + 1e-12, (k, err, np.abs(r).max())
+            d = state[k].astype(np.float64) - sd[k].astype(np.float64)
+            dr = state_ref[k].astype(np.float64) - sd[k].astype(np.float64)
+            big = np.abs(r) >= 1e-3 * np.abs(r).max()
+            assert np.abs(d - dr)[big].max(initial=0) <= 2e-3 * lr, (k, np.abs(d - dr)[big].max())
+        d = state[k].astype(np.float64) - sd[k].astype(np.float64)
+        assert np.abs(d).max() <= lr * 1.01, k
+    for k, v in state_ref.items():
+        if "running" in k:
+            np.testing.assert_allclose(state[k], v, rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_train_step_vs_reference_golden(lib):
+    """The fixture's two steps (the reference's own IKPoseTrainer): step-1 loss, the
+    forward, the step-1 backward + Adam against the oracle (pinned to the same
+    fixture) on the fixture batch, then the step-2 loss and running stats."""
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    g = golden("train.npz")
+    sd = _weights()
+    lr = float(g["lr"])
+    tr = GpuTrainer(_model(sd, 9), lr=lr)
+    x0, t0, m0 = g["x"][0], g["target"][0], g["mask"][0]
+    loss0 = float(tr.step(torch.from_numpy(x0).cuda(), torch.from_numpy(t0).cuda(), torch.from_numpy(m0).cuda()))
+    np.testing.assert_allclose(loss0, g["loss"][0], rtol=1e-5)
+    _check_forward(tr, sd, x0, m0)
+    _check_step(tr, sd, x0, t0, m0, lr, loss0)
+    loss1 = float(tr.step(torch.from_numpy(g["x"][1]).cuda(), torch.from_numpy(g["target"][1]).cuda(),
+                          torch.from_numpy(g["mask"][1]).cuda()))
+    np.testing.assert_allclose(loss1, g["loss"][1], rtol=1e-3)
+    state = tr.state_dict()
+    for k in g.files:
+        if k.startswith("buf|"):
+            # after two steps: the step-2 batch statistics inherit the +-lr rounding-noise updates above
+            np.testing.assert_allclose(state[k[4:]].cpu().numpy(), g[k], rtol=1e-3, atol=1e-4, err_msg=k)
+    assert int(state["backbone.data_bn.num_batches_tracked"]) == 2
+
+
+@pytest.mark.parametrize("N,T,seed", [(8, 9, 11), (64, 9, 12), (6, 17, 13), (3, 64, 14)])
+def test_train_step_vs_oracle(lib, N, T, seed):
+    """One step: forward, then every gradient and every updated parameter in full."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    sd = _weights()
+    rng = np.random.default_rng(seed)
+    x = syn.synthetic_windows(N, T, seed=seed)
+    Tp = _frames(T)[-1]
+    tgt = rng.normal(0, 0.5, (N, Tp, 66)).astype(np.float32)
+    mask = (rng.random((N * Tp, 512)) < 0.3).astype(np.float32)
+    tr = GpuTrainer(_model(sd, T), lr=1e-4)
+    loss = float(tr.step(torch.from_numpy(x).cuda(), torch.from_numpy(tgt).cuda(), torch.from_numpy(mask).cuda()))
+    _check_forward(tr, sd, x, mask)
+    _check_step(tr, sd, x, tgt, mask, 1e-4, loss)
+
+
+def test_train_steps_converge_and_export(lib):
+    """Repeated steps on one batch drive the loss down (device dropout masks); the
+    exported state dict drops into eval-mode inference (the weight ABI)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    sd = _weights()
+    x = torch.from_numpy(syn.synthetic_windows(32, 9, seed=5)).cuda()
+    tgt = torch.from_numpy(np.random.default_rng(5).normal(0, 0.3, (32, 1, 66)).astype(np.float32)).cuda()
+    m = _model(sd, 9)
+    tr = GpuTrainer(m, lr=1e-3)
+    losses = [float(tr.training_step({"keypoints_3d": x, "poses": tgt}, i)["loss"]) for i in range(30)]
+    assert np.isfinite(losses).all()
+    assert np.mean(losses[-5:]) < 0.5 * np.mean(losses[:3]), losses
+    tr.load_into(m)
+    m = m.cuda().eval()
+    with torch.no_grad():
+        y = m(x)["poses"]
+    st = {k: v.detach().cpu().numpy() for k, v in m.regressor.state_dict().items()}
+    ref = orc.pose_regressor(x.cpu().numpy(), st)["poses"]
+    assert np.abs(y.cpu().numpy() - ref).max() < 1e-4
+
+
+def test_device_dropout_mask_rate(lib):
+    """The counter-based dropout draw keeps ~30 % of the head's activations, and a
+    different seed draws a different mask. With one output row, column j of the
+    second Linear's weight gradient (dO^T D) is zero exactly where D = LeakyReLU(P)
+    * mask / 0.3 is, i.e. where the draw dropped unit j."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    tr = GpuTrainer(_model(_weights(), 9), lr=1e-4)
+    x = torch.from_numpy(syn.synthetic_windows(1, 9, seed=1)).cuda()
+    tgt = torch.zeros((1, 1, 66), device="cuda")
+    kept = []
+    for seed in (123, 456):
+        tr.step(x, tgt, seed=seed)
+        kept.append((tr.tensor("pose_regressor.3.weight", "grad").abs().sum(0) > 0).cpu().numpy())
+    for k in kept:
+        assert 0.2 < k.mean() < 0.4, k.mean()
+    assert (kept[0] != kept[1]).mean() > 0.2
+
+
+def test_train_step_errors(lib):
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    tr = GpuTrainer(_model(_weights(), 9), lr=1e-4)
+    x = torch.zeros((2, 9, 17, 3), device="cuda")
+    with pytest.raises(ValueError):
+        tr.step(x, torch.zeros((2, 2, 66), device="cuda"))
+    with pytest.raises(ValueError):
+        tr.step(torch.zeros((2, 9, 16, 3), device="cuda"), torch.zeros((2, 1, 66), device="cuda"))
+    with pytest.raises(RuntimeError):
+        tr.step(x.cpu(), torch.zeros((2, 1, 66)))

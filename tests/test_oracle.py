@@ -117,3 +117,36 @@ def test_amass_oracle_mapping_and_generator():
     sizes = w.max(1) - w.min(1)
     assert sig.shape == (17, 3) and sig.dtype == np.float32
     assert np.allclose(sig, np.outer(oa.coco_kps_sigma(), sizes.mean(0)) * 0.003, rtol=1e-6)
+
+
+def _golden_train_compare(g, grads, state, sd, rel=1e-3):
+    """max relative error of every stored gradient / two-step change vs the fixture."""
+    worst = 0.0
+    for k in map(str, g["param_names"]):
+        for kind, arr in (("grad", grads[k]), ("delta", state[k].astype(np.float64) - sd[k].astype(np.float64))):
+            key = f"{kind}|{k}"
+            a = np.asarray(arr, np.float64).ravel()
+            if key in g.files:
+                ref, got = g[key], a
+            else:
+                ref, got = g[key + "|val"], a[g[key + "|idx"]]
+                np.testing.assert_allclose(a.sum(), g[key + "|sum"], rtol=1e-3, atol=1e-6 * a.size, err_msg=key)
+            err = float(np.abs(got - ref).max() / (np.abs(ref).max() + 1e-30))
+            assert err < rel, (key, err)
+            worst = max(worst, err)
+    return worst
+
+
+def test_train_step_oracle_vs_reference_golden(ik_weights):
+    """oracle/train.py (torch CPU autograd restatement) against two optimizer steps of
+    the reference's own IKPoseTrainer (tests/golden/make_golden_train.py)."""
+    from oracle import train as otr
+    g = golden("train.npz")
+    assert syn.state_dict_sha256(ik_weights) == str(g["weights_sha256"])
+    batches = [(g["x"][s], g["target"][s], g["mask"][s]) for s in range(g["x"].shape[0])]
+    losses, grads, state = otr.train_steps(ik_weights, batches, lr=float(g["lr"]))
+    np.testing.assert_allclose(losses, g["loss"], rtol=1e-6)
+    assert _golden_train_compare(g, grads, state, ik_weights, rel=1e-5) < 1e-5
+    for k in g.files:
+        if k.startswith("buf|"):
+            np.testing.assert_allclose(state[k[4:]], g[k], rtol=1e-6, atol=1e-7, err_msg=k)

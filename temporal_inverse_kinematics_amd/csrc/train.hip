@@ -368,9 +368,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (long long r = r0; r < r1; r += 16) {
+    // rows r .. r+15 of A and B into registers (zero past the chunk / matrix edge)
+    auto load = [&](long long r, f32x4& av, f32x4& bv) {
+        av = f32x4{0.f, 0.f, 0.f, 0.f};
+        bv = f32x4{0.f, 0.f, 0.f, 0.f};
         const long long row = r + lr;
-        f32x4 av = {0.f, 0.f, 0.f, 0.f}, bv = {0.f, 0.f, 0.f, 0.f};
         if (row < r1) {
             const float* ap = A + row * lda + m0 + c4;
             const float* bp = B + row * ldb + n0 + c4;
@@ -381,10 +383,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
             else
                 for (int e = 0; e < 4; ++e) bv[e] = (n0 + c4 + e < N) ? bp[e] : 0.f;
         }
+    };
+    f32x4 av, bv;
+    load(r0, av, bv);
+    for (long long r = r0; r < r1; r += 16) {
         __syncthreads();
         *reinterpret_cast<f32x4*>(As + lr * LDS_LD + c4) = av;
         *reinterpret_cast<f32x4*>(Bs + lr * LDS_LD + c4) = bv;
         __syncthreads();
+        // the next 16 rows' global loads are in flight during this step's MFMAs
+        if (r + 16 < r1) load(r + 16, av, bv);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const int k = kk * 4 + (lane >> 4);

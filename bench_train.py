@@ -77,6 +77,10 @@ def main():
            "config": {"workload": f"IKPoseTrainer step, bs={B} x {T}-frame windows -> {Tp} output frame(s), Adam lr 1e-4",
                       "batch": B, "window_frames": T},
            "algorithmic_tflops": round(fl * B / dt / 1e12, 2), "mflop_per_window": round(fl / 1e6, 2),
+           "roofline": {"scope": "whole step (forward + backward GEMM FLOPs / step time)", "bound": "mfma",
+                        "achieved": round(fl * B / dt / 1e12, 2), "peak": 157.3, "unit": "TFLOP/s",
+                        "frac": round(fl * B / dt / 1e12 / 157.3, 4),
+                        "peak_basis": "dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md"},
            "loss_last": float(loss)}
     if not a.no_cpu_baseline:
         from oracle import train as otr

@@ -27,5 +27,8 @@ timeout -k 10 300 python bench_stream.py --frames 3000 > $OUT/stream_$TAG.json 2
 cat $OUT/stream_$TAG.json; echo "stream rc=$rc"; [ $rc -eq 0 ] || exit $rc
 echo "== fk"
 timeout -k 10 300 python bench_fk.py > $OUT/fk_$TAG.json 2> $OUT/fk_$TAG.err; rc=$?
-cat $OUT/fk_$TAG.json; echo "fk rc=$rc"
+cat $OUT/fk_$TAG.json; echo "fk rc=$rc"; [ $rc -eq 0 ] || exit $rc
+echo "== train"
+timeout -k 10 300 python bench_train.py > $OUT/train_$TAG.json 2> $OUT/train_$TAG.err; rc=$?
+cat $OUT/train_$TAG.json; echo "train rc=$rc"
 exit 0

@@ -43,9 +43,15 @@ hipError_t launch_mix(float* out, const float* in, const float* A, int trans, lo
 hipError_t launch_mix_grad(const float* Y, const float* dZ, long long frames, int C, const float* A, float* dE,
                            double* part, int max_chunks, hipStream_t st);
 // C[m][n] = sum_r A[r][m] B[r][n] (weight gradients), fp32 MFMA, rows split
-// over workgroups with deterministic partial sums in `part` (>= splits*M*N)
+// over workgroups with deterministic partial sums in `part` (>= splits*M*N).
+// Tap mode (taps.C > 0): B is a temporal conv's input (rows (nw*tin + t)*V + v
+// of C floats, C % 64 == 0), read through the conv's row map (implicit
+// im2col, N = kt*C), and C[m][ci*kt + tap] receives the torch weight layout.
+struct WgradTaps {
+    int C = 0, kt = 1, s = 1, pad = 0, tin = 1, tout = 1, V = 1;
+};
 hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M, int N, long long R, float* C,
-                        int ldc, float* part, long long part_cap, hipStream_t st);
+                        int ldc, float* part, long long part_cap, hipStream_t st, const WgradTaps& taps = WgradTaps());
 // col[r][ci*kt + tap] = src[(n*tin + s*t + tap - pad)*V + v][ci] (0 outside the window)
 hipError_t launch_im2col(float* col, const float* src, int lds, int C, int kt, int s, int pad, int N, int tin,
                          int tout, int V, hipStream_t st);
@@ -54,6 +60,19 @@ hipError_t launch_upsample(float* up, const float* src, int C, int s, int N, int
 // dst[i0*ds0 + i1*ds1 + i2*ds2] = src[soff + i0*ss0 + i1*ss1 + i2*ss2] (weight repacking)
 hipError_t launch_permute(float* dst, const float* src, int d0, int d1, int d2, long long ds0, long long ds1,
                           long long ds2, long long soff, long long ss0, long long ss1, long long ss2, hipStream_t st);
+// A batch of re-layouts in one launch: dst[i0*ds0 + i1*ds1 + i2*ds2] =
+// src[s] (* src2[s] when src2 != null), s = soff + i0*ss0 + i1*ss1 + i2*ss2.
+struct PermDesc {
+    float* dst;
+    const float* src;
+    const float* src2;
+    int d0, d1, d2;
+    long long ds0, ds1, ds2, soff, ss0, ss1, ss2;
+    long long block0;   // first workgroup (permute_batch_blocks)
+};
+// assigns block ranges; returns the grid size
+long long permute_batch_blocks(PermDesc* descs, int nd);
+hipError_t launch_permute_batch(const PermDesc* descs_dev, int nd, long long blocks, hipStream_t st);
 // dst = a * b elementwise (n)
 hipError_t launch_mul(float* dst, const float* a, const float* b, int n, hipStream_t st);
 // dropout keep mask (1 with probability keep, else 0) from a counter-based hash of (seed, i)

@@ -349,9 +349,13 @@ hipError_t launch_mix_grad(const float* Y, const float* dZ, long long frames, in
 // floats of one row and the four groups land on distinct banks). MFMA
 // operands: A-op lane l = A^T[m = l&15][k = l>>4] = As[k][m], B-op =
 // Bs[k][n]; D lane l holds rows 4(l>>4)+e, column l&15.
+// Tap mode (g.C > 0): B is the conv input itself, read through the temporal
+// conv's row map (implicit im2col): column n = tap*C + ci of row r is
+// B[(nw*tin + s*t + tap - pad)*V + v][ci] (zero outside the window), r =
+// (nw*tout + t)*V + v; a 64-column tile never straddles taps (C % 64 == 0).
 __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                     int ldb, int M, int N, long long R, long long rows_per,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ part, WgradTaps g) {
     constexpr int LDS_LD = 80;
     __shared__ float As[16 * LDS_LD];
     __shared__ float Bs[16 * LDS_LD];
@@ -363,6 +367,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
     const int lr = tid >> 4, c4 = (tid & 15) * 4;
     const bool avec = (lda % 4 == 0) && (m0 + c4 + 3 < M);
     const bool bvec = (ldb % 4 == 0) && (n0 + c4 + 3 < N);
+    const int tap = g.C ? n0 / g.C : 0;
+    const int bcol = g.C ? n0 - tap * g.C : n0;
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -373,15 +379,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
         av = f32x4{0.f, 0.f, 0.f, 0.f};
         bv = f32x4{0.f, 0.f, 0.f, 0.f};
         const long long row = r + lr;
+        long long brow = row;
+        bool bok = true;
+        if (g.C && row < r1) {
+            const int v = (int)(row % g.V);
+            const long long q = row / g.V;
+            const int t = (int)(q % g.tout);
+            const long long nw = q / g.tout;
+            const int ts = g.s * t + tap - g.pad;
+            bok = ts >= 0 && ts < g.tin;
+            brow = (nw * g.tin + ts) * g.V + v;
+        }
         if (row < r1) {
             const float* ap = A + row * lda + m0 + c4;
-            const float* bp = B + row * ldb + n0 + c4;
+            const float* bp = B + brow * ldb + bcol + c4;
             if (avec) av = *reinterpret_cast<const f32x4*>(ap);
             else
                 for (int e = 0; e < 4; ++e) av[e] = (m0 + c4 + e < M) ? ap[e] : 0.f;
-            if (bvec) bv = *reinterpret_cast<const f32x4*>(bp);
-            else
+            if (!bok) {
+            } else if (bvec) {
+                bv = *reinterpret_cast<const f32x4*>(bp);
+            } else {
                 for (int e = 0; e < 4; ++e) bv[e] = (n0 + c4 + e < N) ? bp[e] : 0.f;
+            }
         }
     };
     f32x4 av, bv;
@@ -420,7 +440,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
             }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int M, int N, float* C, int ldc) {
+// sum of the row-split partials; tap mode stores column tap*C + ci at ci*kt + tap
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int M, int N, float* C, int ldc,
+                                    int tapC, int kt) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long long)M * N) return;
     const size_t st = (size_t)M * N;
@@ -433,12 +455,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, 
         s3 += part[(size_t)(z + 3) * st + i];
     }
     for (; z < splits; ++z) s0 += part[(size_t)z * st + i];
-    C[(i / N) * ldc + i % N] = (s0 + s1) + (s2 + s3);
+    const int n = (int)(i % N);
+    const int col = tapC ? (n % tapC) * kt + n / tapC : n;
+    C[(i / N) * ldc + col] = (s0 + s1) + (s2 + s3);
 }
 
 hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M, int N, long long R, float* C,
-                        int ldc, float* part, long long part_cap, hipStream_t st) {
+                        int ldc, float* part, long long part_cap, hipStream_t st, const WgradTaps& g) {
     if (M <= 0 || N <= 0) return hipSuccess;
+    if (g.C && (g.C % 64 || N != g.kt * g.C || g.V <= 0 || g.tout <= 0)) return hipErrorInvalidValue;
     const int gx = (M + 63) / 64, gy = (N + 63) / 64;
     long long splits = 512 / (gx * gy);
     const long long max_by_rows = (R + 255) / 256;   // >= 256 rows per split
@@ -451,9 +476,9 @@ hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M,
     if (rows_per < 16) rows_per = 16;
     splits = R > 0 ? (R + rows_per - 1) / rows_per : 1;
     hipLaunchKernelGGL(wgrad_kernel, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, A, lda, B, ldb, M, N, R,
-                       rows_per, part);
+                       rows_per, part, g);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nblk((long long)M * N, 256)), dim3(256), 0, st, part, (int)splits, M,
-                       N, C, ldc);
+                       N, C, ldc, g.C, g.kt);
     return hipGetLastError();
 }
 
@@ -522,6 +547,40 @@ hipError_t launch_permute(float* dst, const float* src, int d0, int d1, int d2, 
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(permute_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, dst, src, d0, d1, d2, ds0, ds1, ds2, soff,
                        ss0, ss1, ss2);
+    return hipGetLastError();
+}
+
+// every weight re-layout of a step in one launch: workgroup b serves the
+// descriptor whose block range holds b (ranges laid out by the host)
+__global__ __launch_bounds__(256) void permute_batch_kernel(const PermDesc* __restrict__ descs, int nd) {
+    int d = 0;
+    while (d + 1 < nd && descs[d + 1].block0 <= (long long)blockIdx.x) ++d;
+    const PermDesc& q = descs[d];
+    const long long n = (long long)q.d0 * q.d1 * q.d2;
+    for (long long i = (blockIdx.x - q.block0) * 1024LL + threadIdx.x, e = 0; e < 4; ++e, i += 256) {
+        if (i >= n) return;
+        const int i2 = (int)(i % q.d2);
+        const long long r = i / q.d2;
+        const int i1 = (int)(r % q.d1);
+        const int i0 = (int)(r / q.d1);
+        const long long so = q.soff + i0 * q.ss0 + i1 * q.ss1 + i2 * q.ss2;
+        const float v = q.src[so];
+        q.dst[i0 * q.ds0 + i1 * q.ds1 + i2 * q.ds2] = q.src2 ? v * q.src2[so] : v;
+    }
+}
+
+long long permute_batch_blocks(PermDesc* descs, int nd) {
+    long long b = 0;
+    for (int d = 0; d < nd; ++d) {
+        descs[d].block0 = b;
+        b += ((long long)descs[d].d0 * descs[d].d1 * descs[d].d2 + 1023) / 1024;
+    }
+    return b;
+}
+
+hipError_t launch_permute_batch(const PermDesc* descs_dev, int nd, long long blocks, hipStream_t st) {
+    if (nd == 0 || blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(permute_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, st, descs_dev, nd);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -84,6 +85,9 @@ struct tik_trainer {
     DevIBuf cmap0;
     long long partf_cap = 0, partd_cap = 0;
     long long steps = 0;
+    DevArray<unsigned char> perm;   // weight re-layout descriptors (tik::PermDesc)
+    int nperm = 0;
+    long long perm_blocks = 0;
     std::vector<DevBuf> dbg_dx;   // TIK_TRAIN_DEBUG=1: each block's input gradient of the last step
     DevBuf dbg_b[5];              // TIK_TRAIN_DEBUG_LAYER=l: that block's gS, dU, dH (post-ReLU), dZ, dY
     float lr = 1e-4f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, momentum = 0.1f;
@@ -114,26 +118,43 @@ int add_entry(tik_trainer* t, const TensorMap& m, const std::string& name, int k
 
 const HostTensor* shape_of(const TensorMap& m, const std::string& k) { return find(m, k); }
 
-// GEMM-side layouts from the flat parameters (after create and every update)
+// GEMM-side layouts from the flat parameters (after create and every update):
+// one batched launch over a descriptor table built once (pointers are fixed)
 int derive(tik_trainer* t, hipStream_t st) {
-    const float* P = t->P.p;
-    for (TLayer& l : t->L) {
-        const int ci = l.cin, cp = l.cinp, co = l.cout;
-        // wgf[co][cp] <- W[co][ci]; wgb[ci][co] <- W[co][ci]
-        HIP_TRY(tik::launch_permute(l.wgf.p, P + l.wg, co, ci, 1, cp, 1, 0, 0, ci, 1, 0, st));
-        HIP_TRY(tik::launch_permute(l.wgb.p, P + l.wg, ci, co, 1, co, 1, 0, 0, 1, ci, 0, st));
-        // wtf[co][tap][c] <- W[co][c][tap]; wtb[c][tap'][co] <- W[co][c][2 - tap']
-        HIP_TRY(tik::launch_permute(l.wtf.p, P + l.wt, co, 3, co, 3LL * co, co, 1, 0, 3LL * co, 1, 3, st));
-        HIP_TRY(tik::launch_permute(l.wtb.p, P + l.wt, co, 3, co, 3LL * co, co, 1, 2, 3, -1, 3LL * co, st));
-        if (l.res == RES_C) {
-            HIP_TRY(tik::launch_permute(l.wrf.p, P + l.wr, co, ci, 1, cp, 1, 0, 0, ci, 1, 0, st));
-            HIP_TRY(tik::launch_permute(l.wrb.p, P + l.wr, ci, co, 1, co, 1, 0, 0, 1, ci, 0, st));
+    if (!t->perm.p) {
+        const float* P = t->P.p;
+        std::vector<tik::PermDesc> d;
+        auto add = [&](float* dst, const float* src, const float* src2, int d0, int d1, int d2, long long ds0,
+                       long long ds1, long long ds2, long long soff, long long ss0, long long ss1, long long ss2) {
+            tik::PermDesc q{dst, src, src2, d0, d1, d2, ds0, ds1, ds2, soff, ss0, ss1, ss2, 0};
+            d.push_back(q);
+        };
+        for (TLayer& l : t->L) {
+            const int ci = l.cin, cp = l.cinp, co = l.cout;
+            // wgf[co][cp] <- W[co][ci]; wgb[ci][co] <- W[co][ci]
+            add(l.wgf.p, P + l.wg, nullptr, co, ci, 1, cp, 1, 0, 0, ci, 1, 0);
+            add(l.wgb.p, P + l.wg, nullptr, ci, co, 1, co, 1, 0, 0, 1, ci, 0);
+            // wtf[co][tap][c] <- W[co][c][tap]; wtb[c][tap'][co] <- W[co][c][2 - tap']
+            add(l.wtf.p, P + l.wt, nullptr, co, 3, co, 3LL * co, co, 1, 0, 3LL * co, 1, 3);
+            add(l.wtb.p, P + l.wt, nullptr, co, 3, co, 3LL * co, co, 1, 2, 3, -1, 3LL * co);
+            if (l.res == RES_C) {
+                add(l.wrf.p, P + l.wr, nullptr, co, ci, 1, cp, 1, 0, 0, ci, 1, 0);
+                add(l.wrb.p, P + l.wr, nullptr, ci, co, 1, co, 1, 0, 0, 1, ci, 0);
+            }
+            // A_eff = A * edge_importance (st_gcn_aaai18.py:129)
+            add(l.aeff.p, t->B.p + t->A, P + l.E, V * V, 1, 1, 1, 0, 0, 0, 1, 0, 0);
         }
-        HIP_TRY(tik::launch_mul(l.aeff.p, t->B.p + t->A, P + l.E, V * V, st));
+        // W1^T [feat][512] <- W1[512][feat]; W2^T [512][ldp] <- W2[pose][512]
+        add(t->w1b.p, P + t->w1, nullptr, t->feat, HIDDEN, 1, HIDDEN, 1, 0, 0, 1, t->feat, 0);
+        add(t->w2b.p, P + t->w2, nullptr, HIDDEN, t->pose_dim, 1, t->ldp, 1, 0, 0, 1, HIDDEN, 0);
+        t->perm_blocks = tik::permute_batch_blocks(d.data(), (int)d.size());
+        t->nperm = (int)d.size();
+        std::vector<unsigned char> bytes(d.size() * sizeof(tik::PermDesc));
+        memcpy(bytes.data(), d.data(), bytes.size());
+        int rc;
+        if ((rc = t->perm.upload(bytes))) return rc;
     }
-    // W1^T [feat][512] <- W1[512][feat]; W2^T [512][ldp] <- W2[pose][512]
-    HIP_TRY(tik::launch_permute(t->w1b.p, P + t->w1, t->feat, HIDDEN, 1, HIDDEN, 1, 0, 0, 1, t->feat, 0, st));
-    HIP_TRY(tik::launch_permute(t->w2b.p, P + t->w2, HIDDEN, t->pose_dim, 1, t->ldp, 1, 0, 0, 1, HIDDEN, 0, st));
+    HIP_TRY(tik::launch_permute_batch(reinterpret_cast<const tik::PermDesc*>(t->perm.p), t->nperm, t->perm_blocks, st));
     return TIK_OK;
 }
 
@@ -214,8 +235,8 @@ int colsum(tik_trainer* t, const float* X, long long R, int C, float* dst, hipSt
 }
 
 int wgrad(tik_trainer* t, const float* A, int lda, const float* Bm, int ldb, int M, int Nn, long long R, float* C,
-          int ldc, hipStream_t st) {
-    HIP_TRY(tik::launch_wgrad(A, lda, Bm, ldb, M, Nn, R, C, ldc, t->partf.p, t->partf_cap, st));
+          int ldc, hipStream_t st, const tik::WgradTaps& g = tik::WgradTaps()) {
+    HIP_TRY(tik::launch_wgrad(A, lda, Bm, ldb, M, Nn, R, C, ldc, t->partf.p, t->partf_cap, st, g));
     return TIK_OK;
 }
 
@@ -274,19 +295,30 @@ int backward_block(tik_trainer* t, TLayer& l, const float* X, int ldx, const flo
         return rc;
     // tcn.2: bias and weight gradients (im2col of H, [ci][tap] = the torch weight layout)
     if ((rc = colsum(t, t->tU.p, pout, co, Gd + l.bt, st))) return rc;
-    HIP_TRY(tik::launch_im2col(t->col.p, l.H.p, co, co, 3, l.stride, 1, N, l.tin, l.tout, V, st));
-    if ((rc = wgrad(t, t->tU.p, co, t->col.p, 3 * co, co, 3 * co, pout, Gd + l.wt, 3 * co, st))) return rc;
+    {
+        // implicit im2col of H through the conv's row map (C % 64 == 0 for every block)
+        tik::WgradTaps g;
+        g.C = co; g.kt = 3; g.s = l.stride; g.pad = 1; g.tin = l.tin; g.tout = l.tout; g.V = V;
+        if (co % 64 == 0) {
+            if ((rc = wgrad(t, t->tU.p, co, l.H.p, co, co, 3 * co, pout, Gd + l.wt, 3 * co, st, g))) return rc;
+        } else {
+            HIP_TRY(tik::launch_im2col(t->col.p, l.H.p, co, co, 3, l.stride, 1, N, l.tin, l.tout, V, st));
+            if ((rc = wgrad(t, t->tU.p, co, t->col.p, 3 * co, co, 3 * co, pout, Gd + l.wt, 3 * co, st))) return rc;
+        }
+    }
     // residual conv: bias and weight gradients
     if (l.res == RES_C) {
         if ((rc = colsum(t, t->tQ.p, pout, co, Gd + l.br, st))) return rc;
-        const float* Xs = X;
-        int ldxs = ldx;
-        if (l.stride != 1) {
+        if (l.stride == 1) {
+            if ((rc = wgrad(t, t->tQ.p, co, X, ldx, co, ci, pout, Gd + l.wr, ci, st))) return rc;
+        } else if (ci % 64 == 0 && ldx == ci) {   // strided rows of X read in place (tap mode, kt = 1)
+            tik::WgradTaps g;
+            g.C = ci; g.kt = 1; g.s = l.stride; g.pad = 0; g.tin = l.tin; g.tout = l.tout; g.V = V;
+            if ((rc = wgrad(t, t->tQ.p, co, X, ldx, co, ci, pout, Gd + l.wr, ci, st, g))) return rc;
+        } else {
             HIP_TRY(tik::launch_im2col(t->col.p, X, ldx, l.cinp, 1, l.stride, 0, N, l.tin, l.tout, V, st));
-            Xs = t->col.p;
-            ldxs = l.cinp;
+            if ((rc = wgrad(t, t->tQ.p, co, t->col.p, l.cinp, co, ci, pout, Gd + l.wr, ci, st))) return rc;
         }
-        if ((rc = wgrad(t, t->tQ.p, co, Xs, ldxs, co, ci, pout, Gd + l.wr, ci, st))) return rc;
     }
     // tcn.2 input gradient: the transposed conv = stride-1 conv of the
     // (zero-upsampled) dU with the tap-flipped, transposed weights

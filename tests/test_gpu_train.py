@@ -215,3 +215,24 @@ def test_train_step_errors(lib):
         tr.step(torch.zeros((2, 9, 16, 3), device="cuda"), torch.zeros((2, 1, 66), device="cuda"))
     with pytest.raises(RuntimeError):
         tr.step(x.cpu(), torch.zeros((2, 1, 66)))
+
+
+def test_train_step_bitwise_reproducible(lib):
+    """Two trainers, same weights and batches: bit-identical losses, gradients and
+    parameters after two steps (fixed-order reductions, no atomics in any sum)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    sd = _weights()
+    x = torch.from_numpy(syn.synthetic_windows(48, 9, seed=21)).cuda()
+    tgt = torch.from_numpy(np.random.default_rng(21).normal(0, 0.5, (48, 1, 66)).astype(np.float32)).cuda()
+    out = []
+    for _ in range(2):
+        tr = GpuTrainer(_model(sd, 9), lr=1e-4)
+        losses = [float(tr.step(x, tgt, seed=s)) for s in (7, 8)]
+        out.append((losses, {k: v.cpu().numpy() for k, v in tr.grads().items()},
+                    {k: v.cpu().numpy() for k, v in tr.state_dict().items()}))
+    assert out[0][0] == out[1][0]
+    for k in out[0][1]:
+        assert np.array_equal(out[0][1][k], out[1][1][k]), k
+    for k in out[0][2]:
+        assert np.array_equal(out[0][2][k], out[1][2][k]), k

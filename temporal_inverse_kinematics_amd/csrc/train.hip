@@ -374,6 +374,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // tap mode: this thread's row r0 + lr decoded once into (window, frame,
+    // joint), then advanced incrementally by 16 rows per step (V = 17 > 16:
+    // at most one joint wrap and one frame wrap per step; no 64-bit divides
+    // in the loop)
+    int tv = 0, tt = 0;
+    long long tn = 0;
+    if (g.C) {
+        const long long row = r0 + lr;
+        tv = (int)(row % g.V);
+        const long long q = row / g.V;
+        tt = (int)(q % g.tout);
+        tn = q / g.tout;
+    }
     // rows r .. r+15 of A and B into registers (zero past the chunk / matrix edge)
     auto load = [&](long long r, f32x4& av, f32x4& bv) {
         av = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -381,14 +394,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ A,
         const long long row = r + lr;
         long long brow = row;
         bool bok = true;
-        if (g.C && row < r1) {
-            const int v = (int)(row % g.V);
-            const long long q = row / g.V;
-            const int t = (int)(q % g.tout);
-            const long long nw = q / g.tout;
-            const int ts = g.s * t + tap - g.pad;
+        if (g.C) {
+            const int ts = g.s * tt + tap - g.pad;
             bok = ts >= 0 && ts < g.tin;
-            brow = (nw * g.tin + ts) * g.V + v;
+            brow = (tn * g.tin + ts) * g.V + tv;
+            tv += 16;
+            if (tv >= g.V) {
+                tv -= g.V;
+                if (++tt >= g.tout) { tt = 0; ++tn; }
+            }
         }
         if (row < r1) {
             const float* ap = A + row * lda + m0 + c4;
@@ -463,7 +477,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, int splits, 
 hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M, int N, long long R, float* C,
                         int ldc, float* part, long long part_cap, hipStream_t st, const WgradTaps& g) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    if (g.C && (g.C % 64 || N != g.kt * g.C || g.V <= 0 || g.tout <= 0)) return hipErrorInvalidValue;
+    if (g.C && (g.C % 64 || N != g.kt * g.C || g.V <= 16 || g.tout <= 0)) return hipErrorInvalidValue;
     const int gx = (M + 63) / 64, gy = (N + 63) / 64;
     long long splits = 512 / (gx * gy);
     const long long max_by_rows = (R + 255) / 256;   // >= 256 rows per split

@@ -197,11 +197,12 @@ int reserve(tik_trainer* t, int N, int T) {
 }
 
 // fp32 implicit GEMM: 128x128 tiles when they fill the chip (>= 256
-// workgroups), else 64x64 tiles (the training batches are 10-40k rows: 128x128
-// tiles would leave most CUs idle)
+// workgroups) and the output is wider than 64 channels, else 64x64 tiles (the
+// training batches are 10-40k rows: 128x128 tiles would leave CUs idle, and
+// half of each tile would be empty on the 64-channel blocks)
 int gemm(const tik::CgemmArgs& a, hipStream_t st) {
     const long long t128 = (long long)((a.M + 127) / 128) * ((a.Nc + 127) / 128);
-    const int cfg = t128 >= 256 ? tik::CFG_T128x128 : tik::CFG_H64x64;
+    const int cfg = (a.Nc > 64 && t128 >= 256) ? tik::CFG_T128x128 : tik::CFG_H64x64;
     HIP_TRY(tik::launch_cgemm(a, cfg, st, tik::PREC_F32));
     return TIK_OK;
 }

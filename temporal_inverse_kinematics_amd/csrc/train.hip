@@ -86,30 +86,30 @@ hipError_t launch_colstats(const float* A, const float* G, const float* mean, lo
     return hipGetLastError();
 }
 
-// sum over chunks of part[z][c][k] for one column: 16 lanes stride the
-// chunks, then a fixed xor-shuffle tree within the 16-lane group
-__device__ __forceinline__ double chunk_sum16(const double* __restrict__ part, int nchunk, int C, int c, int k,
-                                              int lane16) {
+// sum over chunks of part[z][c][k] for one column: the 64 lanes of a wave
+// stride the chunks, then a fixed xor-shuffle tree across the wave
+__device__ __forceinline__ double chunk_sum64(const double* __restrict__ part, int nchunk, int C, int c, int k,
+                                              int lane) {
     double s = 0.0;
-    for (int z = lane16; z < nchunk; z += 16) s += part[((size_t)z * C + c) * 2 + k];
+    for (int z = lane; z < nchunk; z += 64) s += part[((size_t)z * C + c) * 2 + k];
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     return s;
 }
 
-// finalize kernels: 256 threads = 16 columns x 16 chunk lanes
+// finalize kernels: 256 threads = 4 columns, one wave (64 chunk lanes) each
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __restrict__ part, int nchunk, long long R,
                                                               int C, const int* __restrict__ cmap,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float* run_mean,
                                                               float* run_var, float momentum, float eps,
                                                               float* __restrict__ stat) {
-    const int lane16 = threadIdx.x & 15;
-    const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= C) return;
-    const double s1 = chunk_sum16(part, nchunk, C, c, 0, lane16);
-    const double s2 = chunk_sum16(part, nchunk, C, c, 1, lane16);
-    if (lane16) return;
+    const double s1 = chunk_sum64(part, nchunk, C, c, 0, lane);
+    const double s2 = chunk_sum64(part, nchunk, C, c, 1, lane);
+    if (lane) return;
     const int p = cmap ? cmap[c] : c;
     if (p < 0) {
         stat[c] = 0.f; stat[C + c] = 0.f; stat[2 * C + c] = 0.f; stat[3 * C + c] = 0.f;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
 hipError_t launch_bn_fwd_finalize(const double* part, int nchunk, long long R, int C, const int* cmap,
                                   const float* gamma, const float* beta, float* run_mean, float* run_var,
                                   float momentum, float eps, float* stat, hipStream_t st) {
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nblk(C, 16)), dim3(256), 0, st, part, nchunk, R, C, cmap, gamma,
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(nblk(C, 4)), dim3(256), 0, st, part, nchunk, R, C, cmap, gamma,
                        beta, run_mean, run_var, momentum, eps, stat);
     return hipGetLastError();
 }
@@ -145,12 +145,12 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ stat, float* dgamma,
                                                               float* dbeta, float* __restrict__ k) {
-    const int lane16 = threadIdx.x & 15;
-    const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= C) return;
-    const double s1 = chunk_sum16(part, nchunk, C, c, 0, lane16);
-    const double s2 = chunk_sum16(part, nchunk, C, c, 1, lane16);
-    if (lane16) return;
+    const double s1 = chunk_sum64(part, nchunk, C, c, 0, lane);
+    const double s2 = chunk_sum64(part, nchunk, C, c, 1, lane);
+    if (lane) return;
     const int p = cmap ? cmap[c] : c;
     if (p < 0) {
         k[c] = 0.f; k[C + c] = 0.f; k[2 * C + c] = 0.f;
@@ -169,22 +169,22 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 hipError_t launch_bn_bwd_finalize(const double* part, int nchunk, long long R, int C, const int* cmap,
                                   const float* gamma, const float* stat, float* dgamma, float* dbeta, float* k,
                                   hipStream_t st) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C, 16)), dim3(256), 0, st, part, nchunk, R, C, cmap, gamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(nblk(C, 4)), dim3(256), 0, st, part, nchunk, R, C, cmap, gamma,
                        stat, dgamma, dbeta, k);
     return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void colsum_finalize_kernel(const double* __restrict__ part, int nchunk, int C,
                                                               float* dst) {
-    const int lane16 = threadIdx.x & 15;
-    const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= C) return;
-    const double s = chunk_sum16(part, nchunk, C, c, 0, lane16);
-    if (lane16 == 0) dst[c] = (float)s;
+    const double s = chunk_sum64(part, nchunk, C, c, 0, lane);
+    if (lane == 0) dst[c] = (float)s;
 }
 
 hipError_t launch_colsum_finalize(const double* part, int nchunk, int C, float* dst, hipStream_t st) {
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(nblk(C, 16)), dim3(256), 0, st, part, nchunk, C, dst);
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(nblk(C, 4)), dim3(256), 0, st, part, nchunk, C, dst);
     return hipGetLastError();
 }
 
@@ -318,14 +318,14 @@ __global__ __launch_bounds__(256) void mix_grad_kernel(const float* __restrict__
 
 __global__ __launch_bounds__(256) void mix_grad_finalize_kernel(const double* __restrict__ part, int nchunk,
                                                                 const float* __restrict__ A, float* dE) {
-    const int lane16 = threadIdx.x & 15;
-    const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per (v, w)
     if (i >= 289) return;
     double s = 0.0;
-    for (int z = lane16; z < nchunk; z += 16) s += part[(size_t)z * 289 + i];
+    for (int z = lane; z < nchunk; z += 64) s += part[(size_t)z * 289 + i];
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
-    if (lane16 == 0) dE[i] = (float)s * A[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) dE[i] = (float)s * A[i];
 }
 
 hipError_t launch_mix_grad(const float* Y, const float* dZ, long long frames, int C, const float* A, float* dE,
@@ -338,7 +338,7 @@ hipError_t launch_mix_grad(const float* Y, const float* dZ, long long frames, in
     nc = frames > 0 ? (frames + fpc - 1) / fpc : 0;
     if (nc > 0)
         hipLaunchKernelGGL(mix_grad_kernel, dim3((unsigned)nc), dim3(256), 0, st, Y, dZ, frames, C, fpc, part);
-    hipLaunchKernelGGL(mix_grad_finalize_kernel, dim3(nblk(289, 16)), dim3(256), 0, st, part, (int)nc, A, dE);
+    hipLaunchKernelGGL(mix_grad_finalize_kernel, dim3(nblk(289, 4)), dim3(256), 0, st, part, (int)nc, A, dE);
     return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 """Layer-by-layer GPU vs oracle comparison (debug aid)."""
 import sys, os
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np, torch
 from oracle import stgcn as orc
 from temporal_inverse_kinematics_amd import synthetic as syn

@@ -3,7 +3,7 @@ in. Runs the 1024-window batch whole and as sub-batches of several sizes
 (one handle; then S handles on S streams) and reports max |difference|; the
 worst window is checked against the CPU oracle."""
 import sys, os, json
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch
 from temporal_inverse_kinematics_amd import synthetic as syn

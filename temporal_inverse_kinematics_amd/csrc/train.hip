@@ -13,6 +13,8 @@
 // gradients) are column reductions over those rows: 64 consecutive columns
 // per workgroup (coalesced 256-B row segments), rows split over chunks,
 // double partial sums reduced in a fixed order (run-to-run deterministic).
+#include <cstdlib>
+
 #include "train.h"
 
 namespace tik {
@@ -76,7 +78,8 @@ hipError_t launch_colstats(const float* A, const float* G, const float* mean, lo
                            int max_chunks, int* nchunk, hipStream_t st) {
     if (C % 4) return hipErrorInvalidValue;
     const int gx = (C + 63) / 64;
-    long long nc = (R + CS_ROWS - 1) / CS_ROWS;
+    static const int cs_rows = getenv("TIK_CS_ROWS") ? atoi(getenv("TIK_CS_ROWS")) : CS_ROWS;   // A/B knob
+    long long nc = (R + cs_rows - 1) / cs_rows;
     if (nc > max_chunks) nc = max_chunks;
     if (nc < 1) nc = 1;
     const long long rows_per = R > 0 ? (R + nc - 1) / nc : 1;
@@ -479,7 +482,8 @@ hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M,
     if (M <= 0 || N <= 0) return hipSuccess;
     if (g.C && (g.C % 64 || N != g.kt * g.C || g.V <= 16 || g.tout <= 0)) return hipErrorInvalidValue;
     const int gx = (M + 63) / 64, gy = (N + 63) / 64;
-    long long splits = 512 / (gx * gy);
+    static const int target = getenv("TIK_WG_TARGET") ? atoi(getenv("TIK_WG_TARGET")) : 512;   // A/B knob
+    long long splits = target / (gx * gy);
     const long long max_by_rows = (R + 255) / 256;   // >= 256 rows per split
     if (splits > max_by_rows) splits = max_by_rows;
     if (splits > part_cap / ((long long)M * N)) splits = part_cap / ((long long)M * N);

@@ -13,8 +13,9 @@ namespace tik {
 //   G == nullptr: (sum A, sum A^2)
 //   G != nullptr: (sum G, sum G * (A - mean[c]))   (mean may be null -> 0)
 // rows of C floats (ld = C). Returns the chunk count through *nchunk.
+// M (optional, G mode): ReLU backward folded in, g = M > 0 ? G : 0.
 hipError_t launch_colstats(const float* A, const float* G, const float* mean, long long R, int C, double* part,
-                           int max_chunks, int* nchunk, hipStream_t st);
+                           int max_chunks, int* nchunk, hipStream_t st, const float* M = nullptr);
 // train-mode BatchNorm statistics from colstats(A): mean, invstd, scale =
 // gamma*invstd, shift = beta - mean*scale per column into stat[4][C]; running
 // stats updated (momentum, unbiased variance). cmap: column -> channel
@@ -33,8 +34,9 @@ hipError_t launch_colsum_finalize(const double* part, int nchunk, int C, float* 
 hipError_t launch_affine(float* out, const float* X, const float* sc, const float* sh, const float* R2,
                          const float* sc2, const float* sh2, long long R, int C, int relu, hipStream_t st);
 // out = g*k0 + (x - mean)*k1 + k2 (BatchNorm input gradient); stat = bn_fwd_finalize's stat
+// M (optional): g = M > 0 ? G : 0 (ReLU backward folded in)
 hipError_t launch_bn_bwd_apply(float* out, const float* G, const float* X, const float* stat, const float* k,
-                               long long R, int C, hipStream_t st);
+                               long long R, int C, hipStream_t st, const float* M = nullptr);
 // out = M > 0 ? G : 0 (ReLU backward on its output); n elements
 hipError_t launch_relu_bwd(float* out, const float* G, const float* M, long long n, hipStream_t st);
 // out[f][w][c] = sum_v Amat(v, w) in[f][v][c]; Amat = A (trans=0) or A^T (trans=1), V = 17

@@ -29,8 +29,9 @@ static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) 
 // accumulators; the 16 row lanes reduced through LDS in a fixed order.
 constexpr int CS_ROWS = 128;   // rows per chunk
 __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ A, const float* __restrict__ G,
-                                                       const float* __restrict__ mean, long long R, int C,
-                                                       long long rows_per, double* __restrict__ part) {
+                                                       const float* __restrict__ M, const float* __restrict__ mean,
+                                                       long long R, int C, long long rows_per,
+                                                       double* __restrict__ part) {
     __shared__ double red[2][16][64];
     const int tid = threadIdx.x, q = tid & 15, rl = tid >> 4;
     const int c = blockIdx.x * 64 + 4 * q;
@@ -43,7 +44,12 @@ __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__
         for (long long r = r0 + rl; r < r1; r += 16) {
             const f32x4 a = *reinterpret_cast<const f32x4*>(A + r * C + c);
             if (G) {
-                const f32x4 g = *reinterpret_cast<const f32x4*>(G + r * C + c);
+                f32x4 g = *reinterpret_cast<const f32x4*>(G + r * C + c);
+                if (M) {   // ReLU backward folded in: g where the ReLU output is positive
+                    const f32x4 mk = *reinterpret_cast<const f32x4*>(M + r * C + c);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) g[e] = mk[e] > 0.f ? g[e] : 0.f;
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     s1[e] += g[e];
@@ -75,7 +81,7 @@ __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__
 }
 
 hipError_t launch_colstats(const float* A, const float* G, const float* mean, long long R, int C, double* part,
-                           int max_chunks, int* nchunk, hipStream_t st) {
+                           int max_chunks, int* nchunk, hipStream_t st, const float* M) {
     if (C % 4) return hipErrorInvalidValue;
     const int gx = (C + 63) / 64;
     static const int cs_rows = getenv("TIK_CS_ROWS") ? atoi(getenv("TIK_CS_ROWS")) : CS_ROWS;   // A/B knob
@@ -85,7 +91,7 @@ hipError_t launch_colstats(const float* A, const float* G, const float* mean, lo
     const long long rows_per = R > 0 ? (R + nc - 1) / nc : 1;
     nc = R > 0 ? (R + rows_per - 1) / rows_per : 1;
     *nchunk = (int)nc;
-    hipLaunchKernelGGL(colstats_kernel, dim3(gx, (unsigned)nc), dim3(256), 0, st, A, G, mean, R, C, rows_per, part);
+    hipLaunchKernelGGL(colstats_kernel, dim3(gx, (unsigned)nc), dim3(256), 0, st, A, G, M, mean, R, C, rows_per, part);
     return hipGetLastError();
 }
 
@@ -213,19 +219,20 @@ hipError_t launch_affine(float* out, const float* X, const float* sc, const floa
 }
 
 __global__ void bn_bwd_apply_kernel(float* __restrict__ out, const float* __restrict__ G,
-                                    const float* __restrict__ X, const float* __restrict__ stat,
-                                    const float* __restrict__ k, long long n, int C) {
+                                    const float* __restrict__ M, const float* __restrict__ X,
+                                    const float* __restrict__ stat, const float* __restrict__ k, long long n, int C) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int c = (int)(i % C);
-    out[i] = G[i] * k[c] + (X[i] - stat[c]) * k[C + c] + k[2 * C + c];
+    const float g = (!M || M[i] > 0.f) ? G[i] : 0.f;
+    out[i] = g * k[c] + (X[i] - stat[c]) * k[C + c] + k[2 * C + c];
 }
 
 hipError_t launch_bn_bwd_apply(float* out, const float* G, const float* X, const float* stat, const float* k,
-                               long long R, int C, hipStream_t st) {
+                               long long R, int C, hipStream_t st, const float* M) {
     const long long n = R * C;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, out, G, X, stat, k, n, C);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, out, G, M, X, stat, k, n, C);
     return hipGetLastError();
 }
 

@@ -218,13 +218,14 @@ int bn_stats(tik_trainer* t, const float* X, long long R, int C, const int* cmap
 }
 
 // BatchNorm backward: grads of gamma/beta into G, dx into out (when non-null)
+// (Mr: the output of a ReLU between this BatchNorm and Gr, whose backward is folded in)
 int bn_back(tik_trainer* t, const float* Gr, const float* X, long long R, int C, const int* cmap, long long g,
-            long long b, const float* stat, float* out, hipStream_t st) {
+            long long b, const float* stat, float* out, hipStream_t st, const float* Mr = nullptr) {
     int nc = 0;
-    HIP_TRY(tik::launch_colstats(X, Gr, stat, R, C, t->partd.p, (int)(t->partd_cap / (2LL * C)), &nc, st));
+    HIP_TRY(tik::launch_colstats(X, Gr, stat, R, C, t->partd.p, (int)(t->partd_cap / (2LL * C)), &nc, st, Mr));
     HIP_TRY(tik::launch_bn_bwd_finalize(t->partd.p, nc, R, C, cmap, t->P.p + g, stat, t->G.p + g, t->G.p + b,
                                         t->k.p, st));
-    if (out) HIP_TRY(tik::launch_bn_bwd_apply(out, Gr, X, stat, t->k.p, R, C, st));
+    if (out) HIP_TRY(tik::launch_bn_bwd_apply(out, Gr, X, stat, t->k.p, R, C, st, Mr));
     return TIK_OK;
 }
 
@@ -288,11 +289,18 @@ int backward_block(tik_trainer* t, TLayer& l, const float* X, int ldx, const flo
     const long long pin = (long long)N * l.tin * V, pout = (long long)N * l.tout * V;
     float* Gd = t->G.p;
     int rc;
-    // block ReLU
-    HIP_TRY(tik::launch_relu_bwd(t->tS.p, dO, l.O.p, pout * co, st));
+    // block ReLU: materialized (gS) only where the identity residual passes it
+    // on; otherwise folded into the two BatchNorm backward passes
+    const float* gS = dO;
+    const float* mO = l.O.p;
+    if (l.res == RES_I) {
+        HIP_TRY(tik::launch_relu_bwd(t->tS.p, dO, l.O.p, pout * co, st));
+        gS = t->tS.p;
+        mO = nullptr;
+    }
     // tcn.3 BatchNorm -> dU ; residual BatchNorm -> dQ
-    if ((rc = bn_back(t, t->tS.p, l.U.p, pout, co, nullptr, l.g2, l.b2, l.st2.p, t->tU.p, st))) return rc;
-    if (l.res == RES_C && (rc = bn_back(t, t->tS.p, l.Q.p, pout, co, nullptr, l.g3, l.b3, l.st3.p, t->tQ.p, st)))
+    if ((rc = bn_back(t, gS, l.U.p, pout, co, nullptr, l.g2, l.b2, l.st2.p, t->tU.p, st, mO))) return rc;
+    if (l.res == RES_C && (rc = bn_back(t, gS, l.Q.p, pout, co, nullptr, l.g3, l.b3, l.st3.p, t->tQ.p, st, mO)))
         return rc;
     // tcn.2: bias and weight gradients (im2col of H, [ci][tap] = the torch weight layout)
     if ((rc = colsum(t, t->tU.p, pout, co, Gd + l.bt, st))) return rc;
@@ -333,9 +341,8 @@ int backward_block(tik_trainer* t, TLayer& l, const float* X, int ldx, const flo
     h.seg[0] = seg32(du, l.wtb.p, co, co, 3, 1, 1, l.tin, 3 * co);
     h.nseg = 1; h.out = t->tH.p; h.ldo = co; h.act = tik::ACT_NONE;
     if ((rc = gemm(h, st))) return rc;
-    // tcn.1 ReLU, tcn.0 BatchNorm -> dZ
-    HIP_TRY(tik::launch_relu_bwd(t->tH.p, t->tH.p, l.H.p, pin * co, st));
-    if ((rc = bn_back(t, t->tH.p, l.Z.p, pin, co, nullptr, l.g1, l.b1, l.st1.p, t->tZ.p, st))) return rc;
+    // tcn.1 ReLU (folded) + tcn.0 BatchNorm -> dZ
+    if ((rc = bn_back(t, t->tH.p, l.Z.p, pin, co, nullptr, l.g1, l.b1, l.st1.p, t->tZ.p, st, l.H.p))) return rc;
     // graph mix: dY = mix(dZ, A_eff^T); edge-importance gradient
     HIP_TRY(tik::launch_mix(t->tY.p, t->tZ.p, l.aeff.p, 1, (long long)N * l.tin, co, st));
     HIP_TRY(tik::launch_mix_grad(l.Y.p, t->tZ.p, (long long)N * l.tin, co, t->B.p + t->A, Gd + l.E, t->partd.p,
@@ -643,7 +650,8 @@ long long tik_trainer_steps(tik_trainer_t t) { return t ? t->steps : -1; }
 // Debug / test hook on the last step's saved state: which = 0 block `layer`'s
 // output, 2 its tcn conv output U, 3 its ReLU(BN(mix)) H, 4 the mix output Z,
 // 5 the gcn conv output Y (channels-last rows), 6 the head's first Linear
-// output; 1 the block's input gradient and 10..14 its gS, dU, dH, dZ, dY
+// output; 1 the block's input gradient and 10..14 its gS (identity-residual blocks),
+// dU, dH (before the ReLU backward, which is folded into the BatchNorm pass), dZ, dY
 // (recorded with TIK_TRAIN_DEBUG=1 / TIK_TRAIN_DEBUG_LAYER=l). Copies
 // min(n, size) floats to the device pointer dst.
 int tik_trainer_debug(tik_trainer_t t, int which, int layer, float* dst, long long n, void* stream) {

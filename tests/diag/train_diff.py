@@ -90,8 +90,8 @@ if os.environ.get("TIK_TRAIN_DEBUG_LAYER"):
     Ot = F.relu(St)
     Ot.backward(dO)
     def cl(t): return t.detach().permute(0, 2, 3, 1).contiguous().numpy()
-    refs = {2: cl(Ut), 3: cl(Ht), 4: cl(Zt), 5: cl(Yt), 10: cl(St.grad), 11: cl(Ut.grad), 12: cl(Ht.grad * (Ht > 0)), 13: cl(Zt.grad), 14: cl(Yt.grad)}
-    names = {2: "U", 3: "H", 4: "Z", 5: "Y", 10: "gS", 11: "dU", 12: "dH*relu", 13: "dZ", 14: "dY"}
+    refs = {2: cl(Ut), 3: cl(Ht), 4: cl(Zt), 5: cl(Yt), 10: cl(St.grad), 11: cl(Ut.grad), 12: cl(Ht.grad), 13: cl(Zt.grad), 14: cl(Yt.grad)}
+    names = {2: "U", 3: "H", 4: "Z", 5: "Y", 10: "gS", 11: "dU", 12: "dH", 13: "dZ", 14: "dY"}
     for w, r in refs.items():
         o = torch.empty(r.size, device="cuda")
         _lib.check(_lib.load().tik_trainer_debug(tr._h.h, w, L, o.data_ptr(), o.numel(), 0))

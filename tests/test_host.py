@@ -40,6 +40,24 @@ def test_library_rejects_bad_args_without_gpu():
         _lib.check(lib.tik_model_create(arr, 1, _lib.ctypes.byref(h)))
 
 
+def test_trainer_abi_rejects_bad_args_without_gpu():
+    """The training-step C ABI validates before touching the device: a state dict
+    without the layer strides is a KeyError, null handles / bad reads ValueError."""
+    from temporal_inverse_kinematics_amd import _lib
+    lib = _lib.load()
+    arr, keep = _lib.pack_tensors([("backbone.data_bn.weight", np.ones(51, np.float32))])
+    h = _lib.ctypes.c_void_p()
+    with pytest.raises(KeyError, match="tik.strides"):
+        _lib.check(lib.tik_trainer_create(arr, 1, _lib.ctypes.c_float(1e-4), _lib.ctypes.byref(h)))
+    with pytest.raises(ValueError):
+        _lib.check(lib.tik_trainer_create(arr, 1, _lib.ctypes.c_float(0.0), _lib.ctypes.byref(h)))
+    with pytest.raises(ValueError):
+        _lib.check(lib.tik_trainer_step(None, None, 1, 9, None, None, 0, None, None))
+    with pytest.raises(ValueError):
+        _lib.check(lib.tik_trainer_read(None, 0, 0, None, None))
+    assert lib.tik_trainer_steps(None) == -1
+
+
 def test_graph_matches_reference():
     from temporal_inverse_kinematics_amd.st_gcn import Graph
     g = golden("graph.npz")

@@ -198,41 +198,70 @@ hipError_t launch_colsum_finalize(const double* part, int nchunk, int C, float* 
 }
 
 // ---------------------------------------------------------------- elementwise
+// float4 per thread (every C here is a multiple of 4); the channel index from
+// 32-bit arithmetic (element counts stay below 2^31 in float4 units)
 __global__ void affine_kernel(float* __restrict__ out, const float* __restrict__ X, const float* __restrict__ sc,
                               const float* __restrict__ sh, const float* __restrict__ R2,
-                              const float* __restrict__ sc2, const float* __restrict__ sh2, long long n, int C,
+                              const float* __restrict__ sc2, const float* __restrict__ sh2, unsigned n4, unsigned C4,
                               int relu) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = (int)(i % C);
-    float v = X[i] * sc[c] + sh[c];
-    if (R2) v += sc2 ? R2[i] * sc2[c] + sh2[c] : R2[i];
-    out[i] = (relu && !(v > 0.f)) ? 0.f : v;
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const unsigned c = (i % C4) * 4;
+    const f32x4 x = reinterpret_cast<const f32x4*>(X)[i];
+    const f32x4 a = *reinterpret_cast<const f32x4*>(sc + c);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(sh + c);
+    f32x4 v = x * a + b;
+    if (R2) {
+        const f32x4 r = reinterpret_cast<const f32x4*>(R2)[i];
+        if (sc2) v += r * *reinterpret_cast<const f32x4*>(sc2 + c) + *reinterpret_cast<const f32x4*>(sh2 + c);
+        else v += r;
+    }
+    if (relu)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    reinterpret_cast<f32x4*>(out)[i] = v;
 }
 
 hipError_t launch_affine(float* out, const float* X, const float* sc, const float* sh, const float* R2,
                          const float* sc2, const float* sh2, long long R, int C, int relu, hipStream_t st) {
     const long long n = R * C;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(affine_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, out, X, sc, sh, R2, sc2, sh2, n, C, relu);
+    if (C % 4 || n / 4 >= (1LL << 31)) return hipErrorInvalidValue;
+    const unsigned n4 = (unsigned)(n / 4);
+    hipLaunchKernelGGL(affine_kernel, dim3(nblk(n4, 256)), dim3(256), 0, st, out, X, sc, sh, R2, sc2, sh2, n4,
+                       (unsigned)(C / 4), relu);
     return hipGetLastError();
 }
 
 __global__ void bn_bwd_apply_kernel(float* __restrict__ out, const float* __restrict__ G,
                                     const float* __restrict__ M, const float* __restrict__ X,
-                                    const float* __restrict__ stat, const float* __restrict__ k, long long n, int C) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int c = (int)(i % C);
-    const float g = (!M || M[i] > 0.f) ? G[i] : 0.f;
-    out[i] = g * k[c] + (X[i] - stat[c]) * k[C + c] + k[2 * C + c];
+                                    const float* __restrict__ stat, const float* __restrict__ k, unsigned n4,
+                                    unsigned C4) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const unsigned c = (i % C4) * 4, C = C4 * 4;
+    f32x4 g = reinterpret_cast<const f32x4*>(G)[i];
+    if (M) {
+        const f32x4 m = reinterpret_cast<const f32x4*>(M)[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
+    }
+    const f32x4 x = reinterpret_cast<const f32x4*>(X)[i];
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(stat + c);
+    const f32x4 k0 = *reinterpret_cast<const f32x4*>(k + c);
+    const f32x4 k1 = *reinterpret_cast<const f32x4*>(k + C + c);
+    const f32x4 k2 = *reinterpret_cast<const f32x4*>(k + 2 * C + c);
+    reinterpret_cast<f32x4*>(out)[i] = g * k0 + (x - mu) * k1 + k2;
 }
 
 hipError_t launch_bn_bwd_apply(float* out, const float* G, const float* X, const float* stat, const float* k,
                                long long R, int C, hipStream_t st, const float* M) {
     const long long n = R * C;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, out, G, M, X, stat, k, n, C);
+    if (C % 4 || n / 4 >= (1LL << 31)) return hipErrorInvalidValue;
+    const unsigned n4 = (unsigned)(n / 4);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nblk(n4, 256)), dim3(256), 0, st, out, G, M, X, stat, k, n4,
+                       (unsigned)(C / 4));
     return hipGetLastError();
 }
 

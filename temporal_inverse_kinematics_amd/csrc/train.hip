@@ -563,23 +563,26 @@ hipError_t launch_im2col(float* col, const float* src, int lds, int C, int kt, i
     return hipGetLastError();
 }
 
-__global__ void upsample_kernel(float* __restrict__ up, const float* __restrict__ src, int C, int s, long long n_in,
-                                int tin, int tout, int V) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_in * C) return;
-    const long long r = i / C;
-    const int c = (int)(i % C);
-    const int v = (int)(r % V);
-    const long long q = r / V;
-    const int t = (int)(q % tin);
-    const long long n = q / tin;
-    up[i] = (t % s == 0) ? src[((n * tout + t / s) * V + v) * C + c] : 0.f;
+// float4 per thread, 32-bit index arithmetic (counts < 2^31 in float4 units)
+__global__ void upsample_kernel(float* __restrict__ up, const float* __restrict__ src, unsigned C4, int s,
+                                unsigned n4, unsigned tin, unsigned tout, unsigned V) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    const unsigned r = i / C4, c4 = i - r * C4;
+    const unsigned q = r / V, v = r - q * V;
+    const unsigned n = q / tin, t = q - n * tin;
+    f32x4 val = {0.f, 0.f, 0.f, 0.f};
+    if (t % s == 0) val = reinterpret_cast<const f32x4*>(src)[((n * tout + t / s) * V + v) * C4 + c4];
+    reinterpret_cast<f32x4*>(up)[i] = val;
 }
 
 hipError_t launch_upsample(float* up, const float* src, int C, int s, int N, int tin, int tout, int V, hipStream_t st) {
     const long long n_in = (long long)N * tin * V;
     if (n_in * C == 0) return hipSuccess;
-    hipLaunchKernelGGL(upsample_kernel, dim3(nblk(n_in * C, 256)), dim3(256), 0, st, up, src, C, s, n_in, tin, tout, V);
+    if (C % 4 || n_in * C / 4 >= (1LL << 31)) return hipErrorInvalidValue;
+    const unsigned n4 = (unsigned)(n_in * C / 4);
+    hipLaunchKernelGGL(upsample_kernel, dim3(nblk(n4, 256)), dim3(256), 0, st, up, src, (unsigned)(C / 4), s, n4,
+                       (unsigned)tin, (unsigned)tout, (unsigned)V);
     return hipGetLastError();
 }
 

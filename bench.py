@@ -26,8 +26,16 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-in MFMA (= f32 vector) peak
-F16_MFMA_PEAK_TFLOPS = 2516.6   # 1024 FLOP/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz (~2.5 PF dense)
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 / f16 MFMA: 1024 FLOP/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz (~2.5 PF)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
+# MFMA products per fp32 product, and the dense peak of the MFMA that executes them
+ARITH = {"bf16x3": (6, BF16_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x32_bf16"),
+         "f16x3": (3, BF16_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x32_f16"),
+         "fp32": (1, FP32_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x4_f32")}
+DTYPE = {"bf16x3": "f32 via bf16x3 (x = 3 bf16 planes, 6 MFMA products, fp32 accumulate; fp32 exponent range)",
+         "f16x3": "f32 via f16x3 (3 MFMA products; f16 range, narrower than fp32)",
+         "fp32": "f32 (exact fp32 MFMA)"}
+PREC_CODE = {"fp32": 0, "f16x3": 1, "bf16x3": 2}
 
 # profiler label prefix (csrc/api.cpp ProfScope) -> kernel symbol in rocprofv3 output
 KERNEL_SYMBOLS = {
@@ -48,6 +56,19 @@ KERNEL_SYMBOLS = {
 }
 
 
+def kernel_symbol(label, precision):
+    """rocprofv3 symbol of the launch behind a profiler label (register-staged
+    cgemm.hip tiles are templated on the precision code)."""
+    if label in KERNEL_SYMBOLS:
+        return KERNEL_SYMBOLS[label]
+    p = PREC_CODE[precision]
+    nb_graph = 2 if p == 0 else 1
+    cg = {"G272x64": f"272, 64, 1, 4, 1, 17, {p}, {nb_graph}", "T128x128": f"128, 128, 2, 2, 0, 0, {p}, 2",
+          "T128x64": f"128, 64, 2, 2, 0, 0, {p}, 2", "T256x64": f"256, 64, 4, 1, 0, 0, {p}, 2",
+          "H64x64": f"64, 64, 2, 2, 0, 0, {p}, 2"}
+    return f"tik::cgemm_kernel<{cg[label]}>" if label in cg else None
+
+
 def newest_profile(pattern):
     """The newest profiles/`pattern` by the rNN_vMM tag in its name (file
     mtimes are checkout times, not measurement order), or None."""
@@ -61,14 +82,14 @@ def newest_profile(pattern):
     return cands[-1] if cands else None
 
 
-def _pmc_value(path, label, pattern, field):
+def _pmc_value(path, label, pattern, field, precision):
     """`field` of the kernel behind `label` in a PMC summary (scripts/pmc_traffic.py
     or pmc_mfma.py output; default: the newest profiles/`pattern`), or None."""
     if path is None:
         path = newest_profile(pattern)
     if not path or not os.path.exists(path):
         return None, None
-    sym = KERNEL_SYMBOLS.get(label)
+    sym = kernel_symbol(label, precision)
     kern = json.load(open(path)).get("kernels", {})
     for k, v in kern.items():
         name = k.replace("void ", "").strip()
@@ -77,36 +98,63 @@ def _pmc_value(path, label, pattern, field):
     return None, os.path.relpath(path, REPO)
 
 
-def _pmc_traffic(path, label):
+def _pmc_traffic(path, label, precision):
     """HBM bytes per dispatch of the kernel behind `label` (scripts/pmc_traffic.py)."""
-    return _pmc_value(path, label, "*pmc_traffic*.json", "hbm_bytes_per_dispatch")
+    return _pmc_value(path, label, "*pmc_traffic*.json", "hbm_bytes_per_dispatch", precision)
 
 
-def _pmc_mfma(path, label):
+def _pmc_mfma(path, label, precision):
     """MFMA-busy fraction of the kernel behind `label` (scripts/pmc_mfma.py)."""
-    return _pmc_value(path, label, "*pmc_mfma*.json", "mfma_busy_frac")
+    return _pmc_value(path, label, "*pmc_mfma*.json", "mfma_busy_frac", precision)
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def _cpu_baseline(T: int, seconds: float = 12.0):
-    """Oracle (numpy fp32, the reference algorithm unfused) on a bounded sample."""
+    """The reference forward restated with the torch CPU ops the reference runs
+    (oracle/stgcn.py pose_regressor_torch, pinned to the reference's fixtures),
+    fp32, eval, on a bounded sample. Thread count: the best of the CPUs this
+    process may run on (sched_getaffinity) and the box's 16-CPU share, probed
+    briefly; the count used is reported."""
     import numpy as np
-    from threadpoolctl import threadpool_info
+    import torch
 
     from oracle import stgcn as orc
     from temporal_inverse_kinematics_amd import synthetic as syn
     sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
-    nb = 8
+    nb = 16
     x = syn.synthetic_windows(nb, T, seed=7)
-    orc.pose_regressor(x[:1], sd, dtype=np.float32)     # warm
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cands = sorted({max(1, min(16, avail)), avail})
+    best, rate = cands[0], 0.0
+    for n in cands:
+        torch.set_num_threads(n)
+        orc.pose_regressor_torch(x[:2], sd)
+        t0 = time.perf_counter()
+        orc.pose_regressor_torch(x, sd)
+        r = nb / (time.perf_counter() - t0)
+        if r > rate:
+            best, rate = n, r
+    torch.set_num_threads(best)
     done, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        orc.pose_regressor(x, sd, dtype=np.float32)
+        orc.pose_regressor_torch(x, sd)
         done += nb
     dt = time.perf_counter() - t0
-    threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    return {"value": done / dt, "unit": "IK frames/s", "cores": int(threads), "kind": "port",
-            "sample": f"{done} windows (T={T}) of the numpy fp32 oracle (oracle/stgcn.py, pinned to the "
-                      f"reference's fixtures) in {dt:.1f}s on {os.cpu_count()} visible host CPUs"}
+    return {"value": round(done / dt, 1), "unit": "IK frames/s", "cores": int(best), "kind": "port",
+            "cpu_model": _cpu_model(), "visible_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "threads_probed": cands,
+            "sample": f"{done} windows (T={T}, batches of {nb}) of the reference forward restated in torch CPU ops "
+                      f"(oracle/stgcn.py pose_regressor_torch, fp32 eval, pinned to the reference's fixtures) "
+                      f"in {dt:.1f}s on {best} threads"}
 
 
 def main():
@@ -118,9 +166,10 @@ def main():
     ap.add_argument("--T", type=int, default=64, help="frames per window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--precision", default="f16x3", choices=["f16x3", "fp32"],
-                    help="GEMM arithmetic: 3-term f16 split MFMA (default) or exact fp32 MFMA")
-    ap.add_argument("--no-compare", action="store_true", help="skip the second-precision comparison run")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "f16x3"],
+                    help="GEMM arithmetic: bf16x3 (default; fp32 range, 6 bf16 MFMA products), exact fp32 "
+                         "MFMA, or the narrower-range f16x3 split")
+    ap.add_argument("--no-compare", action="store_true", help="skip the other-precision comparison runs")
     ap.add_argument("--no-profile", action="store_true",
                     help="diagnostic: no per-launch HIP events in the timed region (no roofline)")
     ap.add_argument("--pmc-traffic", default=None,
@@ -223,28 +272,30 @@ def main():
 
     ms_step = dt / args.steps * 1e3
     value = world * B / (dt / args.steps)
-    other = None
+    others = []
     if not args.no_compare:
-        # the other arithmetic on the same inputs: time + max |difference| of the poses
-        alt = "fp32" if args.precision == "f16x3" else "f16x3"
+        # the other arithmetics on the same inputs: time + max |difference| of the poses
         with torch.no_grad():
             y_main = reg(x)["poses"].clone()
-            reg.tik_precision = alt
-            y_alt = reg(x)["poses"]
-            for _ in range(2):
-                reg(x)
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                step()
-            torch.cuda.synchronize()
-            dt_alt = time.perf_counter() - t1
+            for alt in [p for p in ("fp32", "f16x3", "bf16x3") if p != args.precision]:
+                reg.tik_precision = alt
+                y_alt = reg(x)["poses"]
+                for _ in range(2):
+                    reg(x)
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                gathers.drain()
+                torch.cuda.synchronize()
+                dt_alt = time.perf_counter() - t1
+                others.append({"precision": alt, "dtype": DTYPE[alt],
+                               "value": round(world * B / (dt_alt / args.steps), 1),
+                               "ms_per_step": round(dt_alt / args.steps * 1e3, 4),
+                               "max_abs_pose_diff_vs_main": float((y_main - y_alt).abs().max().item())})
             reg.tik_precision = args.precision
-        other = {"precision": alt, "value": round(world * B / (dt_alt / args.steps), 1),
-                 "ms_per_step": round(dt_alt / args.steps * 1e3, 4),
-                 "max_abs_pose_diff_vs_main": float((y_main - y_alt).abs().max().item())}
     if rank == 0 and args.no_profile:
         print(json.dumps({"metric": "IK frames/sec (COCO-17->SMPLx pose)", "value": round(value, 1),
                           "ms_per_step": round(ms_step, 4), "note": "diagnostic run without per-launch events"}))
@@ -254,25 +305,21 @@ def main():
         avg_s = tot_ms / cnt / 1e3
         tflops = tot_fl / cnt / avg_s / 1e12
         gbs = tot_by / cnt / avg_s / 1e9
-        if args.precision == "f16x3":
-            mpeak = F16_MFMA_PEAK_TFLOPS / 3
-            basis = ("fp32-equivalent ceiling of the 3-term f16 split: dense f16 MFMA 2516.6 TF / 3 "
-                     "MFMAs per fp32 product; executed MFMA TF/s = 3 x achieved")
-        else:
-            mpeak = FP32_MFMA_PEAK_TFLOPS
-            basis = "dense fp32 MFMA (v_mfma_f32_16x16x4_f32) peak"
-        # the binding roof is the one the kernel is closer to
-        if gbs / HBM_PEAK_GBS > tflops / mpeak:
-            bound, achieved, peak, unit = "hbm", gbs, HBM_PEAK_GBS, "GB/s"
-            basis = "HBM3E spec peak; achieved = algorithmic bytes (4 B per activation element read/written once)"
-        else:
-            bound, achieved, peak, unit = "mfma", tflops, mpeak, "TFLOP/s"
-        traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom)
-        mfma_busy, mfma_src = _pmc_mfma(args.pmc_mfma, dom)
+        # the path is MFMA-bound (~36k FLOP per HBM byte). The roof
+        # is the dense peak of the MFMA that executes the products: bf16x3 runs 6
+        # bf16 MFMA products per fp32 product, so its fp32-equivalent peak is 2516.6/6
+        nprod, xpeak, instr = ARITH[args.precision]
+        bound, achieved, peak, unit = "mfma", tflops, xpeak / nprod, "TFLOP/s"
+        basis = (f"{instr} dense peak {xpeak} TF / {nprod} MFMA products per fp32 product = {xpeak / nprod:.1f} "
+                 f"fp32-equivalent TF; achieved = algorithmic fp32 FLOPs (SURVEY.md §8(d)) / HIP-event launch time")
+        traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom, args.precision)
+        mfma_busy, mfma_src = _pmc_mfma(args.pmc_mfma, dom, args.precision)
         kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
                        "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 2), "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1)}
                    for k, v in agg.items()}
         fwd_flops = sum(v[2] for v in agg.values()) / args.steps
+        win_bytes = T * 17 * 3 * 4 + Tp * 66 * 4
+        hbm_gbs = world * B * win_bytes / (dt / args.steps) / 1e9
         out = {
             "metric": "IK frames/sec (COCO-17->SMPLx pose)",
             "value": round(value, 1),
@@ -284,13 +331,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 via 3xf16-split MFMA, fp32 accumulate" if args.precision == "f16x3" else "f32",
+            "dtype": DTYPE[args.precision],
             "data": "synthetic (AMASS-shaped windows from the sample sequence; seeded synthetic weights)",
             "config": {"workload": f"ST-GCN IK forward, batch={B}x{T}-frame x COCO-17 windows per GPU -> (B,{Tp},66) "
                                    f"SMPL-X pose" + (f", RCCL all-gather of poses over {world} GPUs" if world > 1 else ""),
                        "global_batch": world * B, "window_frames": T, "out_frames": Tp,
                        "parallelism": f"dp{world}" if world > 1 else "single"},
-            "roofline": {"kernel": dom, "symbol": KERNEL_SYMBOLS.get(dom), "bound": bound,
+            "roofline": {"kernel": dom, "symbol": kernel_symbol(dom, args.precision), "bound": bound,
                          "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
                          "frac": round(achieved / peak, 4), "peak_basis": basis,
                          "traffic": None if traffic is None else round(traffic),
@@ -303,14 +350,22 @@ def main():
                          "algorithmic_bytes_per_launch": round(tot_by / cnt),
                          "algorithmic_flops_per_launch": round(tot_fl / cnt),
                          "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,
-                         "tflops": round(tflops, 2), "gbs_algorithmic": round(gbs, 1)},
+                         "executed_mfma_tflops": round(tflops * nprod, 1), "executed_mfma_peak": xpeak,
+                         "activation_gbs": round(gbs, 1), "activation_hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "activation_basis": "the kernel's layer-to-layer activation bytes (4 B per element read "
+                                             "or written once) / launch time, against the HBM3E spec peak"},
+            "hbm": {"bound": "hbm", "achieved": round(hbm_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(hbm_gbs / HBM_PEAK_GBS, 6), "bytes_per_window": win_bytes,
+                    "basis": "SURVEY.md §8(d) algorithmic bytes per IK frame (window in + poses out) x frames/s; "
+                             "BASELINE.json's 'achieved HBM GB/s fraction' (tiny by construction: the path is "
+                             "MFMA-bound)"},
             "forward": {"algorithmic_tflops": round(fwd_flops * args.steps / dt / 1e12, 2),
                         "mflop_per_window": round(fwd_flops / B / 1e6, 2), "kernels": kernels,
                         "launches": {k: {"avg_ms": round(v[0] / v[1], 4), "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 1),
                                          "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 0)} for k, v in per_launch.items()}},
         }
-        if other is not None:
-            out["other_precision"] = other
+        if others:
+            out["other_precisions"] = others
         out["profiled_ms_per_step"] = round(dt_prof / args.steps * 1e3, 4)
         out["timing"] = ("value/ms_per_step: K steps with no instrumentation; roofline/forward: a second pass of "
                          "the same K steps with HIP events around every launch on its stream")

@@ -164,6 +164,10 @@ int tik_stream_path(tik_stream_t s);
  * temporal-conv tasks only)
  * in task order; returns the task count. */
 int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap);
+/* Test hook: mark the dataflow kernel's dependency-timeout flag, as a real
+ * 0.5 s wait timeout would; the next tik_stream_push then fails (that frame's
+ * pose is invalid, the frame is still appended) and the one after it works. */
+int tik_debug_stream_inject_error(tik_stream_t s);
 
 /* ------------------------------------------------------------------------
  * Training-data generation (data half): AmassDataset

@@ -267,3 +267,49 @@ def angle_axis_to_rotation_matrix(aa, dtype=np.float64):
     Rt = np.stack([one, -rz, ry, rz, one, -rx, -ry, rx, one], -1)
     R = np.where((th2 > 1e-6)[:, None], Rn, Rt)
     return R.reshape(-1, 3, 3)
+
+
+# ------------------------------------------------- torch CPU restatement (baseline)
+def pose_regressor_torch(x, p, layers=IK_LAYERS):
+    """PoseRegressor.forward (pose_trainer.py:94-133) in eval mode with the torch
+    CPU ops the reference itself runs: Conv2d via F.conv2d (gconv_origin.py:59,
+    st_gcn_aaai18.py:180-186,199-202), the einsum of gconv_origin.py:61-63,
+    F.batch_norm with running stats, ReLU / LeakyReLU, Linear. fp32. This is
+    bench.py's CPU baseline (torch on all host threads) and is checked against
+    the golden fixtures in tests/test_oracle.py. x: (N,T,V,C) -> (N,T',66)."""
+    import torch
+    import torch.nn.functional as F
+
+    def t(k):
+        return torch.from_numpy(np.ascontiguousarray(p[k], dtype=np.float32))
+
+    def bn(h, k):
+        return F.batch_norm(h, t(k + ".running_mean"), t(k + ".running_var"), t(k + ".weight"), t(k + ".bias"),
+                            training=False, eps=BN_EPS)
+
+    with torch.no_grad():
+        h = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32))
+        N, T, V, C = h.shape
+        h = bn(h.permute(0, 2, 3, 1).reshape(N, V * C, T), "backbone.data_bn")          # st_gcn_aaai18.py:119-122
+        h = h.reshape(N, V, C, T).permute(0, 2, 3, 1).contiguous()                      # :123-125 (N,C,T,V)
+        A = t("backbone.A")
+        for l, (ci, co, s) in enumerate(layers):
+            pre = f"backbone.st_gcn_networks.{l}."
+            Ae = A * t(f"backbone.edge_importance.{l}")
+            if ci == co and s == 1:
+                res = h
+            else:
+                res = bn(F.conv2d(h, t(pre + "residual.0.weight"), t(pre + "residual.0.bias"), stride=(s, 1)),
+                         pre + "residual.1")
+            y = F.conv2d(h, t(pre + "gcn.conv.weight"), t(pre + "gcn.conv.bias"))
+            n, kc, tt, v = y.shape
+            y = torch.einsum("nkctv,kvw->nctw", y.view(n, Ae.shape[0], kc // Ae.shape[0], tt, v), Ae).contiguous()
+            y = F.relu(bn(y, pre + "tcn.0"))
+            y = bn(F.conv2d(y, t(pre + "tcn.2.weight"), t(pre + "tcn.2.bias"), stride=(s, 1), padding=(1, 0)),
+                   pre + "tcn.3")
+            h = F.relu(y + res)
+        n, c, tt, v = h.shape
+        f = h.permute(0, 2, 3, 1).reshape(n * tt, v * c)                                # :131-132
+        hid = F.leaky_relu(F.linear(f, t("pose_regressor.0.weight"), t("pose_regressor.0.bias")), LEAKY_SLOPE)
+        y = F.linear(hid, t("pose_regressor.3.weight"), t("pose_regressor.3.bias"))
+        return y.reshape(n, tt, -1).numpy()

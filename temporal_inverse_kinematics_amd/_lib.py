@@ -62,6 +62,7 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_rotate_root_z": (_I, (_P, _I, _I, ctypes.c_double, _P)),
     "tik_train_windows": (_I, (_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _I, ctypes.c_ulonglong, _P, _P, _P)),
     "tik_debug_stream_trace": (_I, (_P, ctypes.POINTER(ctypes.c_longlong), _I)),
+    "tik_debug_stream_inject_error": (_I, (_P,)),
     "tik_fk_create": (_I, (ctypes.POINTER(TikTensor), _I, _I, ctypes.POINTER(_P))),
     "tik_fk_destroy": (_I, (_P,)),
     "tik_fk_num_joints": (_I, (_P,)),
@@ -100,11 +101,12 @@ def load(path: str = LIB_PATH):
     return lib
 
 
-PRECISIONS = {"fp32": 0, "f32": 0, "f16x3": 1}
+PRECISIONS = {"fp32": 0, "f32": 0, "f16x3": 1, "bf16x3": 2}
 
 
 def precision_code(name: str) -> int:
-    """'fp32' = exact f32 MFMA, 'f16x3' = 3-term f16 split MFMA (see include/tik.h)."""
+    """'fp32' = exact f32 MFMA; 'bf16x3' = 6-product bf16 split MFMA, fp32 range
+    (the default); 'f16x3' = 3-product f16 split, f16 range (see include/tik.h)."""
     if name not in PRECISIONS:
         raise ValueError(f"unknown precision {name!r}; expected one of {sorted(PRECISIONS)}")
     return PRECISIONS[name]

@@ -52,10 +52,11 @@ namespace {
 
 int round4(int c) { return (c + 3) & ~3; }
 
-tik::Seg mkseg(const float* src, const float* w, const SplitW& sw, int cin, int ld, int kt, int stride, int pad,
-               int tin, int ldw) {
+tik::Seg mkseg(const float* src, const float* w, const SplitW& sw, const SplitW3& s3, int cin, int ld, int kt,
+               int stride, int pad, int tin, int ldw) {
     tik::Seg s{src, w, cin, ld, kt, stride, pad, tin, ldw};
     s.whi = sw.hi.p; s.wlo = sw.lo.p; s.cin8 = sw.cin8; s.ldw8 = sw.ldw8;
+    for (int i = 0; i < 3; ++i) s.wb[i] = s3.p[i].p;
     return s;
 }
 
@@ -184,6 +185,7 @@ struct Layer {
     DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
     SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3, register-staged path)
+    SplitW3 s3g, s3t, s3r;  // bf16 planes p0+p1+p2 of wg, wt, wr (PREC_BF16X3)
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     bool mix_sparse = false;
@@ -239,7 +241,8 @@ struct Layer {
                 for (int ci = 0; ci < cin; ++ci) hwr[(size_t)co * cinp + ci] = scr[co] * Wr->v[(size_t)co * cin + ci];
                 hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
             }
-            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)))
+            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)) ||
+                (rc = s3r.build(hwr, cout, 1, cinp, cinp)))
                 return rc;
             if (cin <= 4) {
                 std::vector<float> h0((size_t)cout * cin);
@@ -253,7 +256,8 @@ struct Layer {
         if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
             (rc = biasT.upload(hbt)) || (rc = swg.build(hwg, cout, 1, cinp, cinp)) ||
             (rc = swt.build(hwt, cout, TK, cout, TK * cout)) || (rc = sbg.build(hwg, cout, 1, cinp, cinp)) ||
-            (rc = sbt.build(hwt, cout, TK, cout, TK * cout)))
+            (rc = sbt.build(hwt, cout, TK, cout, TK * cout)) || (rc = s3g.build(hwg, cout, 1, cinp, cinp)) ||
+            (rc = s3t.build(hwt, cout, TK, cout, TK * cout)))
             return rc;
         return TIK_OK;
     }
@@ -267,7 +271,7 @@ struct Layer {
         const int to = tout(tin, stride);
         tik::CgemmArgs g{};
         g.M = N * tin * V; g.Nc = cout; g.V = V; g.tout = tin;
-        g.seg[0] = mkseg(x, wg.p, swg, cinp, ld, 1, 1, 0, tin, cinp);
+        g.seg[0] = mkseg(x, wg.p, swg, s3g, cinp, ld, 1, 1, 0, tin, cinp);
         g.nseg = 1;
         g.bias = bias2.p; g.out = z; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0;
@@ -281,10 +285,10 @@ struct Layer {
 
         tik::CgemmArgs t{};
         t.M = N * to * V; t.Nc = cout; t.V = V; t.tout = to;
-        t.seg[0] = mkseg(z, wt.p, swt, cout, cout, TK, stride, 1, tin, TK * cout);
+        t.seg[0] = mkseg(z, wt.p, swt, s3t, cout, cout, TK, stride, 1, tin, TK * cout);
         t.nseg = 1;
         if (res == RES_CONV) {
-            t.seg[1] = mkseg(x, wr.p, swr, cinp, ld, 1, stride, 0, tin, cinp);
+            t.seg[1] = mkseg(x, wr.p, swr, s3r, cinp, ld, 1, stride, 0, tin, cinp);
             t.nseg = 2;
         } else if (res == RES_IDEN) {
             t.resid = x; t.ldr = ld;
@@ -598,6 +602,7 @@ struct tik_model {
     DevBuf bn_sc, bn_sh;           // data_bn (V*C0)
     DevBuf w0, b0, w3, b3;         // head
     SplitW sw0, sw3;
+    SplitW3 s30, s33;
     SBW sb0, sb3;
     int prec = 1;
     // ws[0]: the handle's workspace (z, z2: ping-pong for the fused T+G launches);
@@ -683,7 +688,7 @@ int tik_debug_check_guards(void) {
     g_err = rep;
     return bad;
 }
-const char* tik_version(void) { return "tik 0.2.0 (gfx950; fp32 MFMA and f16x3 split MFMA with LDS DMA)"; }
+const char* tik_version(void) { return "tik 0.3.0 (gfx950; bf16x3 split MFMA (default, fp32 range), exact fp32 MFMA, f16x3 split MFMA with LDS DMA)"; }
 
 int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out) {
     if (!tensors || n_tensors <= 0 || !out) return fail(TIK_E_INVALID, "tik_model_create: null argument");
@@ -742,8 +747,19 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     const HostTensor* B0 = find(m, "pose_regressor.0.bias");
     const HostTensor* W3 = find(m, "pose_regressor.3.weight");
     const HostTensor* B3 = find(m, "pose_regressor.3.bias");
-    if (!W0 || !B0 || !W3 || !B3) { delete md; return fail(TIK_E_MISSING, "missing pose_regressor.{0,3}.{weight,bias}"); }
     md->feat = V * cin;
+    md->prec = default_precision();
+    if (!W0 && !B0 && !W3 && !B3) {
+        // backbone-only handle (StgGcn18 state dict, st_gcn_aaai18.py:32-133):
+        // tik_backbone_forward only; tik_ik_forward refuses it
+        if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0))) || (rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
+            delete md;
+            return rc;
+        }
+        *out = md;
+        return TIK_OK;
+    }
+    if (!W0 || !B0 || !W3 || !B3) { delete md; return fail(TIK_E_MISSING, "missing pose_regressor.{0,3}.{weight,bias}"); }
     md->hidden = (int)W0->shape[0];
     md->pose_dim = (int)W3->shape[0];
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
@@ -769,7 +785,9 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
         (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
         (rc = md->sb0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
-        (rc = md->sb3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
+        (rc = md->sb3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
+        (rc = md->s30.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
+        (rc = md->s33.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
         delete md;
         return rc;
     }
@@ -810,6 +828,7 @@ int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
 }
 
 void model_retain(tik_model* m) { m->refs.fetch_add(1); }
+int model_pose_dim(const tik_model* m) { return m->pose_dim; }
 void model_release(tik_model* m) {
     if (m->refs.fetch_sub(1) == 1) delete m;
 }
@@ -818,6 +837,7 @@ int model_online_fill(tik_model* m, tik::OnlineArgs& a) {
     static_assert((int)tik::ONR_ZERO == RES_ZERO && (int)tik::ONR_IDEN == RES_IDEN && (int)tik::ONR_CONV == RES_CONV, "");
     const int nl = (int)m->layers.size();
     if (m->V != 17 || m->C0 != 3 || nl > tik::ONL_MAXL) return fail(TIK_E_INVALID, "online kernel: V=17, 3 input channels, <= %d layers", tik::ONL_MAXL);
+    if (m->pose_dim <= 0) return fail(TIK_E_INVALID, "online kernel: backbone-only handle (no pose_regressor weights)");
     a.nl = nl;
     for (int l = 0; l < nl; ++l) {
         const Layer& L = m->layers[l];
@@ -1008,7 +1028,7 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
 static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, float* part, hipStream_t st) {
     tik::CgemmArgs h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->feat, m->feat, 1, 1, 0, rows, m->feat);
+    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->s30, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = hid; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
     h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
     h.partial = part;
@@ -1019,7 +1039,7 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
     }
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
+    p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->s33, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
     p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
     p.partial = part;
@@ -1094,12 +1114,13 @@ extern "C" {
 
 int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream) {
     if (!m || !x || !poses || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: bad arguments");
+    if (m->pose_dim <= 0) return fail(TIK_E_INVALID, "tik_ik_forward: backbone-only handle (no pose_regressor weights)");
     ProfGuard pg(m);
     return model_forward_ws(m, x, N, T, poses, (hipStream_t)stream, m->ws[0], true);
 }
 
 int tik_model_set_precision(tik_model_t m, int prec) {
-    if (!m || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_model_set_precision: bad arguments");
+    if (!m || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_model_set_precision: bad arguments");
     m->prec = prec;
     return TIK_OK;
 }
@@ -1110,7 +1131,7 @@ int tik_model_get_precision(tik_model_t m) {
 }
 
 int tik_block_set_precision(tik_block_t b, int prec) {
-    if (!b || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_block_set_precision: bad arguments");
+    if (!b || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_block_set_precision: bad arguments");
     b->prec = prec;
     return TIK_OK;
 }

@@ -41,6 +41,22 @@ __host__ __device__ constexpr unsigned coco_hop2_mask(int w) {
 template <int PREC> struct PrecCfg;
 template <> struct PrecCfg<PREC_F32> { static constexpr int BK = 16, LDK = 16, ESZ = 4, PLANES = 1; };
 template <> struct PrecCfg<PREC_F16X3> { static constexpr int BK = 32, LDK = 32, ESZ = 2, PLANES = 2; };
+template <> struct PrecCfg<PREC_BF16X3> { static constexpr int BK = 32, LDK = 32, ESZ = 2, PLANES = 3; };
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// x = p0 + p1 + p2, p_i = bf16_rn(residual): v_cvt_pk_bf16_f32 (round to
+// nearest even) on the exact fp32 residuals
+__device__ __forceinline__ void split3(const f32x4 x, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        p0[e] = (__bf16)x[e];
+        const float r1 = x[e] - (float)p0[e];
+        p1[e] = (__bf16)r1;
+        p2[e] = (__bf16)(r1 - (float)p1[e]);
+    }
+}
 
 // byte offset of 16-B chunk c of 64-B row r in a swizzled [rows][64 B] image
 __device__ __forceinline__ int swz_off(int r, int c) { return r * 64 + ((c ^ ((0x1230 >> (4 * ((r >> 2) & 3))) & 3)) << 4); }
@@ -75,8 +91,8 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     constexpr int KQ = BK / 4;
     constexpr int NA4 = BM * KQ;
     constexpr int LA = (NA4 + 255) / 256;
-    // B: F32: BN*KQ float4 slots; F16X3: BN*(2*BK/8) 16-B slots (hi and lo planes)
-    constexpr int BQ = (PREC == PREC_F32) ? KQ : 2 * BK / 8;
+    // B: F32: BN*KQ float4 slots; F16X3 / BF16X3: BN*(PLANES*BK/8) 16-B slots (one run per plane)
+    constexpr int BQ = (PREC == PREC_F32) ? KQ : PC::PLANES * BK / 8;
     constexpr int NB4 = BN * BQ;
     constexpr int LB = (NB4 + 255) / 256;
     int a_q[LA], a_lrow[LA], a_n[LA], a_t[LA], a_w[LA];
@@ -144,7 +160,9 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
             bcin_cur = sg.cin8;
 #pragma unroll
             for (int i = 0; i < LB; ++i) {
-                const unsigned short* base = (b_q[i] < 4) ? sg.whi : sg.wlo;
+                const unsigned short* base;
+                if constexpr (PREC == PREC_F16X3) base = (b_q[i] < 4) ? sg.whi : sg.wlo;
+                else base = (b_q[i] < 4) ? sg.wb[0] : (b_q[i] < 8 ? sg.wb[1] : sg.wb[2]);
                 b_ptr[i] = b_live[i] ? reinterpret_cast<const unsigned char*>(
                                            base + (size_t)(n0 + b_lrow[i]) * sg.ldw8 + tap * sg.cin8 + 8 * (b_q[i] & 3))
                                      : nullptr;
@@ -187,6 +205,23 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
 #pragma unroll
             for (int i = 0; i < LB; ++i)
                 if (tid + i * 256 < NB4) *reinterpret_cast<f32x4*>(Bs + swz_off(b_lrow[i], b_q[i])) = rb[i];
+        } else if constexpr (PREC == PREC_BF16X3) {
+            unsigned char* A0 = base;
+            unsigned char* B0 = A0 + 3 * BM * 64;
+#pragma unroll
+            for (int i = 0; i < LA; ++i)
+                if (tid + i * 256 < NA4) {
+                    bf16x4 p0, p1, p2;
+                    split3(ra[i], p0, p1, p2);
+                    const int off = swz_off(a_lrow[i], a_q[i] >> 1) + 8 * (a_q[i] & 1);
+                    *reinterpret_cast<bf16x4*>(A0 + off) = p0;
+                    *reinterpret_cast<bf16x4*>(A0 + BM * 64 + off) = p1;
+                    *reinterpret_cast<bf16x4*>(A0 + 2 * BM * 64 + off) = p2;
+                }
+#pragma unroll
+            for (int i = 0; i < LB; ++i)
+                if (tid + i * 256 < NB4)
+                    *reinterpret_cast<f32x4*>(B0 + (b_q[i] >> 2) * BN * 64 + swz_off(b_lrow[i], b_q[i] & 3)) = rb[i];
         } else {
             unsigned char* Ahi = base;
             unsigned char* Alo = Ahi + BM * 64;
@@ -241,6 +276,35 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
 #pragma unroll
                     for (int j = 0; j < FN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[k], fb[j][k], acc[i][j], 0, 0, 0);
+            }
+        } else if constexpr (PREC == PREC_BF16X3) {
+            // six products a_i.b_j, i + j <= 2 (the dropped ones are <= 2^-24
+            // relative each), smallest first, one fp32 accumulator
+            const unsigned char* A0 = base;
+            const unsigned char* B0 = A0 + 3 * BM * 64;
+            bf16x8 b0[FN], b1[FN], b2[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int off = swz_off(brow + j * 16, g);
+                b0[j] = *reinterpret_cast<const bf16x8*>(B0 + off);
+                b1[j] = *reinterpret_cast<const bf16x8*>(B0 + BN * 64 + off);
+                b2[j] = *reinterpret_cast<const bf16x8*>(B0 + 2 * BN * 64 + off);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int off = swz_off(arow + i * 16, g);
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A0 + off);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A0 + BM * 64 + off);
+                const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(A0 + 2 * BM * 64 + off);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[j], acc[i][j], 0, 0, 0);
+                }
             }
         } else {
             const unsigned char* Ahi = base;
@@ -470,6 +534,8 @@ static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
     constexpr int NB16 = (EPI == EPI_GRAPH) ? 1 : 2;
     if (prec == PREC_F16X3)
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F16X3, NB16>), g, blk, 0, st, a);
+    else if (prec == PREC_BF16X3)
+        hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_BF16X3, NB16>), g, blk, 0, st, a);
     else
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F32, 2>), g, blk, 0, st, a);
     if (EPI == EPI_BIAS && a.ksplit > 1) {
@@ -505,6 +571,9 @@ hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
     if (prec == PREC_F16X3)
         for (int s = 0; s < a.nseg; ++s)
             if (!a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+    if (prec == PREC_BF16X3)
+        for (int s = 0; s < a.nseg; ++s)
+            if (!a.seg[s].wb[0] || !a.seg[s].wb[1] || !a.seg[s].wb[2]) return hipErrorInvalidValue;
     (void)hipGetLastError();   // drop a stale error left by earlier runtime calls (not ours)
     switch (cfg) {
         case CFG_T128x128: return launch_t<128, 128, 2, 2, EPI_BIAS, 0>(a, prec, st);

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -155,6 +156,54 @@ struct SplitW {
     }
 };
 
+// fp32 -> bf16 bits, round to nearest even (finite inputs; NaN stays NaN)
+inline unsigned short bf16_rne(float x) {
+    unsigned u;
+    memcpy(&u, &x, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (unsigned short)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+    return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+inline float bf16_to_f32(unsigned short b) {
+    const unsigned u = (unsigned)b << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+// x = p0 + p1 + p2 with p_i = bf16_rne(x - p0 - ... - p_{i-1}): exact for
+// normal fp32 x (each plane takes the next 8 significant bits, the
+// residuals are exact in fp32), full fp32 exponent range
+inline void split_bf16x3(float x, unsigned short& p0, unsigned short& p1, unsigned short& p2) {
+    p0 = bf16_rne(x);
+    const float r1 = x - bf16_to_f32(p0);
+    p1 = bf16_rne(r1);
+    const float r2 = r1 - bf16_to_f32(p1);
+    p2 = bf16_rne(r2);
+}
+
+// fp32 weights [Nc][kt][cin] (row stride ldw floats) -> three bf16 planes
+// [Nc][kt][cin8] (cin8 = cin rounded up to 8, zero-filled): w = p0 + p1 + p2
+// (split_bf16x3). The PREC_BF16X3 arithmetic of cgemm.hip.
+struct SplitW3 {
+    DevHBuf p[3];
+    int cin8 = 0, ldw8 = 0;
+    int build(const std::vector<float>& w, int Nc, int kt, int cin, int ldw) {
+        cin8 = (cin + 7) & ~7;
+        ldw8 = kt * cin8;
+        std::vector<unsigned short> h[3];
+        for (auto& v : h) v.assign((size_t)Nc * ldw8, 0);
+        for (int n = 0; n < Nc; ++n)
+            for (int t = 0; t < kt; ++t)
+                for (int c = 0; c < cin; ++c) {
+                    const size_t o = (size_t)n * ldw8 + (size_t)t * cin8 + c;
+                    split_bf16x3(w[(size_t)n * ldw + (size_t)t * cin + c], h[0][o], h[1][o], h[2][o]);
+                }
+        int rc;
+        for (int i = 0; i < 3; ++i)
+            if ((rc = p[i].upload(h[i]))) return rc;
+        return TIK_OK;
+    }
+};
+
 // Split-block ("SB") weights for cgemm3.hip: w[n][tap*cin + ci] (row stride
 // ldw floats) -> [Nc][kt][nblk][64] halves, each 32-channel block stored as
 // [hi(w) x32 | lo(w) = f16(w - hi) x32], zero-padded to whole blocks.
@@ -179,11 +228,14 @@ struct SBW {
     }
 };
 
-// default arithmetic of the GEMMs: TIK_PRECISION=fp32 selects the exact f32
-// MFMA path; anything else the 3-term f16 split (cgemm.hip)
+// default arithmetic of the GEMMs (cgemm.h PREC_*): TIK_PRECISION=fp32 the
+// exact f32 MFMA path, =f16x3 the 3-term f16 split (narrower range); default
+// bf16x3, the 6-product bf16 split with fp32's exponent range
 inline int default_precision() {
     const char* e = getenv("TIK_PRECISION");
-    return (e && (std::string(e) == "fp32" || std::string(e) == "f32")) ? 0 : 1;
+    if (e && (std::string(e) == "fp32" || std::string(e) == "f32")) return 0;
+    if (e && std::string(e) == "f16x3") return 1;
+    return 2;
 }
 
 // One set of activation buffers for the IK forward. A model handle owns two
@@ -210,6 +262,7 @@ void model_release(tik_model* m);   // deletes the model at the last reference
 // the fp32 weights and shapes of the online-IK dataflow kernel (online.h);
 // TIK_E_INVALID when the model is outside what that kernel supports
 int model_online_fill(tik_model* m, tik::OnlineArgs& a);
+int model_pose_dim(const tik_model* m);   // 0 for a backbone-only handle
 
 
 }  // namespace tik_host

@@ -7,7 +7,7 @@
 //   tgemm (TG_128x128)  v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
 //   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// (f16x3 on split-block operands; the fp32 precision runs both GEMMs on cgemm.hip)
+// (f16x3 on split-block operands; fp32 and bf16x3 run both GEMMs on cgemm.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,6 +34,7 @@ struct tik_fk {
     DevBuf PT;         // [3V][KP]
     DevBuf WT;         // [V][KJ]
     SplitW sPT, sWT;   // f16 hi/lo planes (fp32 path's register-staged GEMMs)
+    SplitW3 s3PT, s3WT;   // bf16 planes p0+p1+p2 (bf16x3 register-staged GEMMs)
     SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
@@ -169,7 +170,8 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
         (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||
         (rc = fk->extra.upload(hex)) || (rc = fk->depth.upload(hdepth)) || (rc = fk->bPT.build(PT, 3 * V, 1, KP, KP)) ||
-        (rc = fk->bWT.build(WT, V, 1, KJ, KJ))) {
+        (rc = fk->bWT.build(WT, V, 1, KJ, KJ)) || (rc = fk->s3PT.build(PT, 3 * V, 1, KP, KP)) ||
+        (rc = fk->s3WT.build(WT, V, 1, KJ, KJ))) {
         delete fk;
         return rc;
     }
@@ -187,7 +189,7 @@ int tik_fk_destroy(tik_fk_t fk) {
 }
 
 int tik_fk_set_precision(tik_fk_t fk, int prec) {
-    if (!fk || (prec != 0 && prec != 1)) return fail(TIK_E_INVALID, "tik_fk_set_precision: bad arguments");
+    if (!fk || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_fk_set_precision: bad arguments");
     fk->prec = prec;
     return TIK_OK;
 }
@@ -257,6 +259,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
         g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
         g.seg[0].whi = fk->sPT.hi.p; g.seg[0].wlo = fk->sPT.lo.p; g.seg[0].cin8 = fk->sPT.cin8; g.seg[0].ldw8 = fk->sPT.ldw8;
+        for (int i = 0; i < 3; ++i) g.seg[0].wb[i] = fk->s3PT.p[i].p;
         g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
         HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
 
@@ -264,6 +267,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
         s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
         s.seg[0].whi = fk->sWT.hi.p; s.seg[0].wlo = fk->sWT.lo.p; s.seg[0].cin8 = fk->sWT.cin8; s.seg[0].ldw8 = fk->sWT.ldw8;
+        for (int i = 0; i < 3; ++i) s.seg[0].wb[i] = fk->s3WT.p[i].p;
         s.nseg = 1; s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl;
         HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
     }

@@ -376,6 +376,9 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
             A->count[0] = c + 1;
             A->ticket[0] = 0;
             A->done[0] = 0;
+            // the H1 task (done: every task has run) already published the flag to
+            // pose_host; a timeout must not leak into the next launch's waits
+            A->err[0] = 0;
         }
     }
 }

@@ -152,6 +152,7 @@ extern "C" {
 int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream_t* out) {
     if (!model || win_size <= 0 || !out) return fail(TIK_E_INVALID, "tik_stream_create: bad arguments");
     *out = nullptr;
+    if (model_pose_dim(model) <= 0) return fail(TIK_E_INVALID, "tik_stream_create: backbone-only model handle");
     auto* s = new tik_stream();
     model_retain(model);
     s->model = model;
@@ -212,8 +213,20 @@ int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap) {
 int tik_stream_reset(tik_stream_t s) {
     if (!s) return fail(TIK_E_INVALID, "null stream");
     HIP_TRY(hipMemsetAsync(s->count.p, 0, sizeof(int), s->st));
+    // the dataflow kernel's scheduling state: completion counters, ticket, done, err
+    if (s->online) HIP_TRY(hipMemsetAsync(s->onl_cnt.p, 0, sizeof(int) * s->onl_cnt.n, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
+    s->host_pose[s->pose_dim] = 0.f;
     s->pushed = 0;
+    return TIK_OK;
+}
+
+int tik_debug_stream_inject_error(tik_stream_t s) {
+    if (!s || !s->online) return fail(TIK_E_INVALID, "tik_debug_stream_inject_error: not a dataflow-kernel stream");
+    // err is the last of the scheduling words (setup_online: cnt[cb + 2])
+    const int one = 1;
+    HIP_TRY(hipMemcpyAsync(s->onl_cnt.p + (s->onl_cnt.n - 1), &one, sizeof(int), hipMemcpyHostToDevice, s->st));
+    HIP_TRY(hipStreamSynchronize(s->st));
     return TIK_OK;
 }
 
@@ -227,9 +240,12 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
         if (rc) return rc;
     }
     HIP_TRY(hipStreamSynchronize(s->st));
-    if (s->online && s->host_pose[s->pose_dim] != 0.f)
-        return fail(TIK_E_HIP, "tik_stream_push: the online kernel timed out waiting on a dependency");
-    ++s->pushed;
+    ++s->pushed;   // the step appended the frame to the device ring either way
+    if (s->online && s->host_pose[s->pose_dim] != 0.f) {
+        s->host_pose[s->pose_dim] = 0.f;
+        return fail(TIK_E_HIP, "tik_stream_push: the online kernel timed out waiting on a dependency "
+                               "(this frame's pose is invalid; the stream stays usable)");
+    }
     const int valid = s->pushed > s->h;   // frame pushed-1-h >= 0 solved
     if (valid && pose_host) memcpy(pose_host, s->host_pose, sizeof(float) * s->pose_dim);
     return valid;

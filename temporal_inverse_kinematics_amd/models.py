@@ -47,6 +47,14 @@ class StgConfig:
     temporal_kernel_size: int
 
 
+def _create_model_handle(named):
+    lib = _lib.load()
+    arr, keep = _lib.pack_tensors(named)
+    h = _lib.ctypes.c_void_p()
+    _lib.check(lib.tik_model_create(arr, len(named), _lib.ctypes.byref(h)), "tik_model_create")
+    return _Handle(h.value, lib.tik_model_destroy)
+
+
 def _state_numpy(module: nn.Module, prefix: str = ""):
     out = []
     for k, v in module.state_dict(prefix=prefix).items():
@@ -168,11 +176,47 @@ class StgGcn18(nn.Module):
         self.edge_importance = nn.ParameterList([nn.Parameter(torch.ones(self.A.size()))
                                                  for _ in self.st_gcn_networks])
         self.strides = [layer.temporal_stride for layer in config.layers]
+        self.out_channels = config.layers[-1].out_channels
+        self._tik = None
+        self._tik_key = None
+        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3" | "f16x3"
 
     def out_frames(self, T: int) -> int:
         for s in self.strides:
             T = (T - 1) // s + 1
         return T
+
+    def tik_handle(self):
+        """A backbone-only libtik handle for the current weights (rebuilt when they change)."""
+        if self.training:
+            raise NotImplementedError("the HIP path implements eval-mode inference only; call .eval()")
+        key = _weights_key(self)
+        if self._tik is None or self._tik_key != key:
+            named = _state_numpy(self, prefix="backbone.")
+            named.append(("tik.strides", np.array(self.strides, dtype=np.float32)))
+            self._tik = _create_model_handle(named)
+            self._tik_key = key
+        if self.tik_precision is not None:
+            _lib.check(_lib.load().tik_model_set_precision(self._tik.h, _lib.precision_code(self.tik_precision)))
+        return self._tik.h
+
+    def forward(self, x):
+        """st_gcn_aaai18.py:113-133: x (N,T,V,C) -> (N,T',V*Cout), feature index
+        v*Cout + c (data_bn, the 8 blocks with A * edge_importance, flatten) —
+        one tik_backbone_forward call."""
+        if x.dim() != 4:
+            raise ValueError(f"expected (N,T,V,C) keypoints, got shape {tuple(x.shape)}")
+        N, T, V, C = x.shape
+        To = self.out_frames(T)
+        if N == 0:
+            return torch.empty((0, To, V * self.out_channels), device=x.device, dtype=torch.float32)
+        x = x.contiguous()
+        _lib.require_gpu(x)
+        h = self.tik_handle()
+        feat = torch.empty((N, To, V * self.out_channels), device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().tik_backbone_forward(h, x.data_ptr(), N, T, feat.data_ptr(), _lib.stream_of(x)),
+                   "StgGcn18")
+        return feat
 
 
 class PoseRegressor(nn.Module):
@@ -195,7 +239,7 @@ class PoseRegressor(nn.Module):
                                             nn.Linear(512, self.pose_dim))
         self._tik = None
         self._tik_key = None
-        self.tik_precision = None   # None: library default; "fp32" | "f16x3"
+        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3" | "f16x3"
 
     def tik_handle(self):
         """The libtik model handle for the current weights (rebuilt when they change)."""
@@ -203,13 +247,9 @@ class PoseRegressor(nn.Module):
             raise NotImplementedError("the HIP path implements eval-mode inference only; call .eval()")
         key = _weights_key(self)
         if self._tik is None or self._tik_key != key:
-            lib = _lib.load()
             named = _state_numpy(self)
             named.append(("tik.strides", np.array(self.backbone.strides, dtype=np.float32)))
-            arr, keep = _lib.pack_tensors(named)
-            h = _lib.ctypes.c_void_p()
-            _lib.check(lib.tik_model_create(arr, len(named), _lib.ctypes.byref(h)), "PoseRegressor")
-            self._tik = _Handle(h.value, lib.tik_model_destroy)
+            self._tik = _create_model_handle(named)
             self._tik_key = key
         if self.tik_precision is not None:
             _lib.check(_lib.load().tik_model_set_precision(self._tik.h, _lib.precision_code(self.tik_precision)))
@@ -222,9 +262,9 @@ class PoseRegressor(nn.Module):
         To = self.backbone.out_frames(T)
         if N == 0:   # an empty batch (e.g. an empty rank shard): empty poses, as torch would give
             return {"poses": torch.empty((0, To, self.pose_dim), device=x.device, dtype=torch.float32)}
-        h = self.tik_handle()
         x = x.contiguous()
         _lib.require_gpu(x)
+        h = self.tik_handle()
         poses = torch.empty((N, To, self.pose_dim), device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().tik_ik_forward(h, x.data_ptr(), N, T, poses.data_ptr(), _lib.stream_of(x)),
                    "PoseRegressor")
@@ -285,5 +325,19 @@ class IKPoseTrainer(nn.Module):
             hp = h if h is not None else default_hparams()
         model = cls(hp)
         sd = ck["state_dict"] if "state_dict" in ck else ck
-        model.load_state_dict(sd, strict=False)
+        model.load_checked_state_dict(sd)
         return model
+
+    def load_checked_state_dict(self, sd):
+        """load_state_dict that fails loudly on any key mismatch. The only keys
+        allowed to be absent are BatchNorm `num_batches_tracked` counters
+        (checkpoints from torch versions before they existed); eval never reads
+        them. A `regressor.` prefix is required, as in the reference's Lightning
+        checkpoints (IKPoseTrainer.regressor, pose_trainer.py:139)."""
+        res = self.load_state_dict(sd, strict=False)
+        missing = [k for k in res.missing_keys if not k.endswith("num_batches_tracked")]
+        if missing or res.unexpected_keys:
+            raise KeyError(f"checkpoint does not match IKPoseTrainer: missing {missing[:8]}"
+                           f"{'...' if len(missing) > 8 else ''} ({len(missing)}), unexpected "
+                           f"{list(res.unexpected_keys)[:8]} ({len(res.unexpected_keys)})")
+        return res

@@ -6,9 +6,9 @@ betas, left_hand_pose, right_hand_pose, transl, ...)` -> `.joints`
 (B,144,3), `.vertices` (B,10475,3); `.faces`, `.batch_size`).
 
 All arithmetic runs in libtik.so (tik_fk_*): the kinematic chain (one wave
-per body), the blend-shape GEMM and the skinning GEMM (f16x3 split MFMA on
-split-block operands by default; exact fp32 MFMA with precision="fp32"), the
-landmark gather.
+per body), the blend-shape GEMM and the skinning GEMM (bf16x3 split MFMA, fp32 range,
+by default; exact fp32 MFMA with precision="fp32"; the narrower f16x3 split
+on split-block operands with precision="f16x3"), the landmark gather.
 The fixed `batch_size` of smplx (which forces the reference to zero-pad
 chunks, smpl_util.py:49-56) is kept as an attribute only: any batch runs.
 Model files: SMPLX_{MALE,FEMALE,NEUTRAL}.npz (licensed, not shipped) are read
@@ -89,9 +89,10 @@ class SMPLX:
         self._destroy = lib.tik_fk_destroy
         if precision is not None:
             _lib.check(lib.tik_fk_set_precision(self._h, _lib.precision_code(precision)))
-        # the GEMM arithmetic in use (library default f16x3 unless TIK_PRECISION=fp32)
+        # the GEMM arithmetic in use (library default bf16x3 unless TIK_PRECISION says otherwise)
+        env = os.environ.get("TIK_PRECISION")
         self.precision = precision if precision is not None else (
-            "fp32" if os.environ.get("TIK_PRECISION") in ("fp32", "f32") else "f16x3")
+            "fp32" if env in ("fp32", "f32") else ("f16x3" if env == "f16x3" else "bf16x3"))
         self.num_joints = _lib.check(lib.tik_fk_num_joints(self._h))
         self.num_verts = _lib.check(lib.tik_fk_num_verts(self._h))
 

@@ -1,0 +1,93 @@
+"""The drop-in boundary on the host (no GPU): the INTEGRATION.md module shim
+resolves the reference's own import lines to the engine, StgGcn18 has its
+own forward, and the Lightning checkpoint reader loads strictly
+(pose_trainer.py:240-256, inference.py:135-137)."""
+import argparse
+import os
+import re
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+
+SHIM_NAMES = ("mmskeleton.ops.st_gcn", "mmskeleton.models", "mmskeleton.models.backbones",
+              "mmskeleton.models.backbones.st_gcn_aaai18")
+
+
+def _shim_source():
+    """The python block of INTEGRATION.md §1 (the one-file shim), verbatim."""
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", text, re.S)
+    shim = [b for b in blocks if "mmskeleton_shim" in b]
+    assert len(shim) == 1
+    return shim[0]
+
+
+def test_integration_shim_resolves_reference_imports():
+    saved = {k: sys.modules.get(k) for k in SHIM_NAMES}
+    try:
+        exec(compile(_shim_source(), "mmskeleton_shim.py", "exec"), {})
+        # the reference's own import lines (st_gcn_aaai18.py:5, pose_trainer.py:16)
+        ns = {}
+        exec("from mmskeleton.ops.st_gcn import ConvTemporalGraphical, Graph\n"
+             "from mmskeleton.models import StgGcn18, StgLayerConfig, StgConfig\n"
+             "from mmskeleton.models.backbones.st_gcn_aaai18 import StGcnBlock, StgGcn18 as S2\n", ns)
+        from temporal_inverse_kinematics_amd import models, st_gcn
+        assert ns["ConvTemporalGraphical"] is st_gcn.ConvTemporalGraphical
+        assert ns["Graph"] is st_gcn.Graph
+        assert ns["StgGcn18"] is models.StgGcn18 and ns["S2"] is models.StgGcn18
+        assert ns["StGcnBlock"] is models.StGcnBlock
+        assert ns["StgLayerConfig"] is models.StgLayerConfig and ns["StgConfig"] is models.StgConfig
+        # PoseRegressor.forward calls self.backbone(x) (pose_trainer.py:101): StgGcn18 must define forward
+        assert "forward" in models.StgGcn18.__dict__
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+
+
+def test_stggcn18_forward_refuses_cpu_tensor():
+    from temporal_inverse_kinematics_amd.models import PoseRegressor, default_hparams
+    reg = PoseRegressor(default_hparams(9)).eval()
+    with pytest.raises((RuntimeError, ValueError)):
+        reg.backbone(torch.zeros(1, 9, 17, 3))
+    assert reg.backbone.out_frames(64) == 4 and reg.backbone.out_channels == 256
+
+
+def _lightning_ckpt(tmp_path, sd, hparams, prefix="regressor.", drop=None):
+    state = {prefix + k: torch.from_numpy(np.asarray(v)) for k, v in sd.items() if k != drop}
+    path = tmp_path / "checkpoint_epoch=98.ckpt"
+    torch.save({"epoch": 98, "state_dict": state, "hparams": hparams}, path)
+    return str(path)
+
+
+@pytest.mark.parametrize("hp_kind", ["namespace", "dict"])
+def test_checkpoint_reader_loads_reference_layout(tmp_path, ik_weights, hp_kind):
+    from temporal_inverse_kinematics_amd.models import IKPoseTrainer, default_hparams
+    hp = default_hparams(64)
+    path = _lightning_ckpt(tmp_path, ik_weights, hp if hp_kind == "namespace" else vars(hp))
+    m = IKPoseTrainer.load_from_checkpoint(path)
+    assert m.hparams.win_size == 64
+    got = m.regressor.state_dict()
+    for k, v in ik_weights.items():
+        assert torch.equal(got[k], torch.from_numpy(np.asarray(v))), k
+
+
+def test_checkpoint_reader_is_strict(tmp_path, ik_weights):
+    from temporal_inverse_kinematics_amd.models import IKPoseTrainer, default_hparams
+    hp = default_hparams(64)
+    with pytest.raises(KeyError):   # wrong prefix: nothing would load
+        IKPoseTrainer.load_from_checkpoint(_lightning_ckpt(tmp_path, ik_weights, hp, prefix="model."))
+    with pytest.raises(KeyError):   # one weight missing
+        IKPoseTrainer.load_from_checkpoint(
+            _lightning_ckpt(tmp_path, ik_weights, hp, drop="backbone.st_gcn_networks.3.tcn.2.weight"))
+    extra = dict(ik_weights)
+    extra["backbone.st_gcn_networks.9.gcn.conv.weight"] = np.zeros((1,), np.float32)
+    with pytest.raises(KeyError):   # a key the module does not have
+        IKPoseTrainer.load_from_checkpoint(_lightning_ckpt(tmp_path, extra, hp))
+    assert isinstance(hp, argparse.Namespace)

@@ -13,10 +13,11 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
+@pytest.fixture(scope="module", params=["bf16x3", "fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
                                                  "f16x3-layered", "f16x3-nofuse", "f16x3-dmahead"])
 def model(request):
-    """fp32 MFMA; f16x3 with the default GEMM path (split-block activations with
+    """bf16x3 (the default: 6-product bf16 split, fp32 range); fp32 MFMA;
+    f16x3 with the default GEMM path (split-block activations with
     LDS DMA at every size, the head as a split-K GEMM on fp32 features when it
     has few rows); and each f16x3 path forced at every size."""
     import os
@@ -104,7 +105,7 @@ def test_run_inference_sample(model):
     assert np.abs(y9 - r["win9"]).max() < TOL
 
 
-@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32", "f16x3"])
 def test_blocks_vs_golden(prec):
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.models import StGcnBlock
@@ -183,7 +184,8 @@ def test_model_dma_subbatches_past_2gib(model):
     assert (y[pick] - solo).abs().max().item() < 2e-5
 
 
-def test_concurrent_streams_bitwise():
+@pytest.mark.parametrize("prec", ["bf16x3", "f16x3"])
+def test_concurrent_streams_bitwise(prec):
     """Four model handles on four HIP streams running concurrently give the
     same poses, bit for bit, as the serial runs (regression: layer 0's graph
     mix once read its constants as broadcast LDS loads and returned wrong
@@ -194,7 +196,7 @@ def test_concurrent_streams_bitwise():
     x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=0)).cuda()
     parts = list(x.chunk(S))
     with torch.no_grad():
-        models = [synthetic_model(win_size=64, device="cuda").regressor for _ in range(S)]
+        models = [synthetic_model(win_size=64, device="cuda", precision=prec).regressor for _ in range(S)]
         ref = [models[i](parts[i])["poses"].clone() for i in range(S)]
         torch.cuda.synchronize()
         streams = [torch.cuda.Stream() for _ in range(S)]
@@ -221,10 +223,10 @@ def test_fused_gcn_epilogue_bitwise():
     import os
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.inference import synthetic_model
-    fused = synthetic_model(win_size=64, device="cuda").regressor
+    fused = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
     os.environ["TIK_FUSE_TG"] = "0"
     try:
-        plain = synthetic_model(win_size=64, device="cuda").regressor
+        plain = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
         plain.tik_handle()
     finally:
         del os.environ["TIK_FUSE_TG"]
@@ -241,10 +243,10 @@ def test_two_stream_split_bitwise():
     import os
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.inference import synthetic_model
-    split = synthetic_model(win_size=64, device="cuda").regressor
+    split = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
     os.environ["TIK_SPLIT"] = "0"
     try:
-        one = synthetic_model(win_size=64, device="cuda").regressor
+        one = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
         one.tik_handle()
     finally:
         del os.environ["TIK_SPLIT"]
@@ -254,13 +256,15 @@ def test_two_stream_split_bitwise():
             assert torch.equal(split(x)["poses"], one(x)["poses"]), n
 
 
-def _model_with_env(**env):
+def _model_with_env(precision="f16x3", **env):
+    """A model whose handle is built under `env` (the f16x3 split-block DMA
+    kernels' switches by default)."""
     import os
     from temporal_inverse_kinematics_amd.inference import synthetic_model
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
     try:
-        m = synthetic_model(win_size=64, device="cuda").regressor
+        m = synthetic_model(win_size=64, device="cuda", precision=precision).regressor
         m.tik_handle()   # env hooks are read at handle creation
     finally:
         for k, v in old.items():
@@ -292,7 +296,7 @@ def test_two_stream_split_repeated_bitwise():
     bit-identical to the one-stream result."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.inference import synthetic_model
-    split = synthetic_model(win_size=64, device="cuda").regressor
+    split = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
     one = _model_with_env(TIK_SPLIT=0)
     x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=11)).cuda()
     with torch.no_grad():
@@ -370,3 +374,43 @@ def test_persistent_gcn_gpw_bitwise():
             y = gpw(x)["poses"]
             assert torch.equal(y, g3(x)["poses"]), (n, T)
             assert torch.equal(gpw_l(x)["poses"], g3_l(x)["poses"]), (n, T)
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+def test_stggcn18_forward_vs_golden(prec):
+    """the reference's PoseRegressor.forward calls
+    self.backbone(x) (pose_trainer.py:101); StgGcn18.forward
+    (st_gcn_aaai18.py:113-133) runs on its own backbone-only handle and
+    matches the golden features; the head applied to them gives the golden
+    poses, i.e. the reference's own forward composes with the engine."""
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    m = golden("model.npz")
+    model = synthetic_model(win_size=64, device="cuda", precision=prec)
+    model.regressor.backbone.tik_precision = prec
+    for T in (64, 65, 9):
+        x = torch.from_numpy(m[f"T{T}|x"]).cuda()
+        with torch.no_grad():
+            feat = model.regressor.backbone(x)
+            n, w, c = feat.shape
+            y = model.regressor.pose_regressor(feat.reshape(n * w, c)).reshape(n, w, -1)
+        assert feat.shape == m[f"T{T}|feat"].shape
+        assert np.abs(feat.cpu().numpy() - m[f"T{T}|feat"]).max() < TOL, T
+        assert np.abs(y.cpu().numpy() - m[f"T{T}|y"]).max() < TOL, T
+
+
+def test_checkpoint_poses_vs_golden(tmp_path):
+    """a Lightning-shaped checkpoint of the seeded weights
+    ({'state_dict': {'regressor.' + k}, 'hparams': Namespace}) loaded with
+    IKPoseTrainer.load_from_checkpoint (strict) solves the golden windows."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.models import IKPoseTrainer, default_hparams
+    sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
+    path = tmp_path / "checkpoint_epoch=98-val_loss=0.02.ckpt"
+    torch.save({"state_dict": {"regressor." + k: torch.from_numpy(v) for k, v in sd.items()},
+                "hparams": default_hparams(64)}, path)
+    model = IKPoseTrainer.load_from_checkpoint(str(path)).cuda().eval()
+    m = golden("model.npz")
+    for T in (64, 9):
+        with torch.no_grad():
+            y = model(torch.from_numpy(m[f"T{T}|x"]).cuda())["poses"].cpu().numpy()
+        assert np.abs(y - m[f"T{T}|y"]).max() < TOL, T

@@ -121,3 +121,37 @@ def test_stream_survives_batch_calls_and_rebuilds():
     assert np.abs(OnlineIK(m, use_graph=True).run(seq) - moved).max() < 1e-5
     del online
     gc.collect()
+
+
+def test_online_timeout_recovers():
+    """a dependency timeout in the dataflow kernel (forced
+    here through tik_debug_stream_inject_error) fails that push only: the
+    frame is still appended (host and device frame counts stay in step), the
+    error flag is cleared for the next launch, and the stream keeps matching
+    run_inference afterwards; reset() clears everything."""
+    from temporal_inverse_kinematics_amd import _build, _lib
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import run_inference, synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    r = golden("run_inference.npz")
+    seq = r["seq"][:40]
+    m = synthetic_model(win_size=9, device="cuda")
+    ref = run_inference(m, seq)
+    s = OnlineIK(m, use_graph=True)
+    assert s.path == "dataflow"
+    lib = _lib.load()
+    s.reset()
+    got = {}
+    for i, fr in enumerate(seq):
+        if i == 10:
+            _lib.check(lib.tik_debug_stream_inject_error(s._s))
+            with pytest.raises(RuntimeError):
+                s.push(fr)
+            continue
+        p = s.push(fr)
+        if p is not None:
+            got[i - s.h] = p
+    for i, p in got.items():
+        if i != 10 - s.h:
+            assert np.abs(p - ref[i]).max() < 1e-5, i
+    assert np.array_equal(s.run(seq), OnlineIK(m, use_graph=True).run(seq))

@@ -93,6 +93,14 @@ def test_pose_regressor(ik_weights, T):
     np.testing.assert_allclose(y, m[f"T{T}|y"], atol=1e-5)
 
 
+@pytest.mark.parametrize("T", [64, 9])
+def test_pose_regressor_torch_baseline(ik_weights, T):
+    """bench.py's CPU baseline (the torch restatement) against the reference's fixture."""
+    m = golden("model.npz")
+    y = orc.pose_regressor_torch(m[f"T{T}|x"], ik_weights)
+    np.testing.assert_allclose(y, m[f"T{T}|y"], atol=2e-5)
+
+
 def test_run_inference_win9(ik_weights):
     r = golden("run_inference.npz")
     y = orc.run_inference(r["seq"], ik_weights, 9)

@@ -27,6 +27,7 @@
 #include "misc.h"
 #include "online.h"
 #include "common.h"
+#include "xgemm.h"
 
 namespace tik_host {
 thread_local std::string g_err;
@@ -188,6 +189,8 @@ struct Layer {
     SplitW3 s3g, s3t, s3r;  // bf16 planes p0+p1+p2 of wg, wt, wr (PREC_BF16X3)
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
+    DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
+    int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -228,6 +231,7 @@ struct Layer {
                     hwt[(size_t)co * TK * cout + tap * cout + ci] = sc2[co] * Wt->v[((size_t)co * cout + ci) * TK + tap];
             hbt[co] = (float)((double)sc2[co] * (bt ? bt->v[co] : 0.0) + sh2[co]);
         }
+        std::vector<float> wr_host;   // folded residual conv [cout][cinp] (RES_CONV)
         if (res == RES_CONV) {
             const HostTensor* Wr = find(m, pre + "residual.0.weight");
             const HostTensor* br = find(m, pre + "residual.0.bias");
@@ -241,6 +245,7 @@ struct Layer {
                 for (int ci = 0; ci < cin; ++ci) hwr[(size_t)co * cinp + ci] = scr[co] * Wr->v[(size_t)co * cin + ci];
                 hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
             }
+            wr_host = hwr;
             if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)) ||
                 (rc = s3r.build(hwr, cout, 1, cinp, cinp)))
                 return rc;
@@ -249,6 +254,20 @@ struct Layer {
                 for (int co = 0; co < cout; ++co)
                     for (int ci = 0; ci < cin; ++ci) h0[(size_t)co * cin + ci] = hwr[(size_t)co * cinp + ci];
                 if ((rc = wr0.upload(h0))) return rc;
+            }
+        }
+        {   // bf16x3 tiles for xgemm.hip
+            const int bn = cout >= 128 ? 128 : 64;
+            if (cin % 32 == 0) {
+                const tik::XPackSeg g{hwg.data(), cinp, 1, cin};
+                if ((rc = xg.upload(tik::xgemm_pack(&g, 1, cout, bn)))) return rc;
+                xg_bn = bn; xg_ks = cin / 32;
+            }
+            if (cout % 32 == 0) {
+                tik::XPackSeg t[2] = {{hwt.data(), TK * cout, TK, cout}, {wr_host.data(), cinp, 1, cin}};
+                const int ns = (res == RES_CONV && cin % 32 == 0) ? 2 : 1;
+                if ((rc = xt.upload(tik::xgemm_pack(t, ns, cout, bn)))) return rc;
+                xt_bn = bn; xt_ks = TK * cout / 32 + (ns == 2 ? cin / 32 : 0);
             }
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
@@ -312,6 +331,60 @@ struct Layer {
             ProfScope p(lab.c_str(), fl, by, st);
             HIP_TRY(tik::launch_cgemm(t, cfg, st, prec));
         }
+        return TIK_OK;
+    }
+
+    bool x_ok() const { return xt.p && (xg.p || (index == 0 && cin <= 4 && res == RES_CONV && wr0.p)); }
+
+    // bf16x3 on fp32 activations (xgemm.hip). x: fp32 rows [N*tin*V][ld];
+    // z: workspace; out: [N*tout*V][cout]. Layer 0 from the raw keypoints
+    // (cin <= 4): xraw = (N,T,V,C0) keypoints, its data_bn'd copy goes to xb4
+    // ([rows][4]) for the residual conv in the temporal conv's epilogue.
+    int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st,
+                  const float* xraw = nullptr, const float* bn_sc = nullptr, const float* bn_sh = nullptr,
+                  float* xb4 = nullptr) const {
+        const int to = tout(tin, stride);
+        const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
+        const double px_in = (double)rin, px_out = (double)rout;
+        if (xraw) {
+            ProfScope p("G0f_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout, 4.0 * (px_in * cin + px_in * cout), st);
+            HIP_TRY(tik::launch_gcn0_f32(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
+                                         cout, z, cout, xb4, st));
+        } else {
+            tik::XArgs g{};
+            g.M = (int)rin; g.Nc = cout; g.V = V; g.tout = tin;
+            g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
+            g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
+            g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
+            const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
+            ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                        4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+            p.out(z, (size_t)rin * cout * 4);
+            HIP_TRY(tik::launch_xgemm(g, xg_bn, tik::EPI_GRAPH, st));
+        }
+        tik::XArgs t{};
+        t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
+        t.seg[0] = tik::XSeg{z, cout, cout, TK, stride, 1, tin, rin};
+        t.nseg = 1;
+        double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
+        if (xraw) {
+            t.rx = xb4; t.rxc = cin; t.rw = wr0.p;
+            fl += 2.0 * px_out * cin * cout; by += 4.0 * px_out * 4;
+        } else if (res == RES_CONV) {
+            t.seg[1] = tik::XSeg{x, ld, cin, 1, stride, 0, tin, rin};
+            t.nseg = 2;
+            fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout);
+        } else if (res == RES_IDEN) {
+            t.resid = x; t.ldr = ld;
+            by += 4.0 * px_out * cout;
+        }
+        t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
+        if (t.ksteps != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, t.ksteps, xt_ks);
+        t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
+        const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
+        ProfScope p(lab.c_str(), fl, by, st);
+        p.out(out, (size_t)rout * cout * 4);
+        HIP_TRY(tik::launch_xgemm(t, xt_bn, tik::EPI_BIAS, st));
         return TIK_OK;
     }
 
@@ -629,6 +702,7 @@ struct tik_model {
     bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
     bool tgw = true;                   // stride-1 fused blocks on the weight-stationary kernel (TIK_TGW=0: TG3)
     bool gpw = true;                   // unfused gcn launches on the persistent kernel (TIK_GPW=0: G3_272x128)
+    bool xgemm = true;                 // bf16x3 backbone on xgemm.hip (TIK_XGEMM=0: register-staged cgemm.hip)
     DevHBuf trash;                     // scratch line for the tgw kernel's stores of invalid rows
     Profiler prof;
     bool profiling = false;
@@ -774,6 +848,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
     if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
     if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
+    if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
@@ -925,6 +1000,48 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
     return TIK_OK;
 }
 
+static bool use_x(const tik_model* m) {
+    if (m->prec != tik::PREC_BF16X3 || !m->xgemm || m->C0 > 4) return false;
+    for (const Layer& L : m->layers)
+        if (!L.x_ok() || (L.index == 0) != (L.cin <= 4)) return false;
+    return true;
+}
+
+// Windows per xgemm call: every fp32 activation tensor the DMA reads stays
+// below 2 GiB (32-bit buffer offsets).
+static int x_chunk(const tik_model* m, int T) {
+    long long worst = 1;
+    int t = T;
+    for (const Layer& L : m->layers) {
+        worst = std::max(worst, (long long)t * m->V * L.cout * 4);   // z
+        t = Layer::tout(t, L.stride);
+        worst = std::max(worst, (long long)t * m->V * L.cout * 4);   // out
+    }
+    const long long lim = (1LL << 31) - (1LL << 20);
+    const int c = (int)std::max(1LL, lim / worst);
+    return m->dma_chunk_max > 0 ? std::min(c, m->dma_chunk_max) : c;
+}
+
+// Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
+// from the raw keypoints (data_bn folded into its gcn kernel).
+static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st,
+                      const WsPtrs& w) {
+    const float* cur = nullptr;
+    int ld = 0, t = T, rc;
+    float* bufs[2] = {w.a0, w.a1};
+    int which = 0;
+    for (const Layer& L : m->layers) {
+        float* o = bufs[which];
+        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb);
+        else rc = L.forward_x(cur, ld, N, t, w.z, o, st);
+        if (rc) return rc;
+        cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
+    }
+    *feat_out = const_cast<float*>(cur);
+    *tout = t;
+    return TIK_OK;
+}
+
 // Backbone on split-block f16 activations (f16x3, large batches): every
 // layer reads and writes SB rows, operands reach LDS by DMA. Returns the
 // features (SB rows of the last layer) and their row stride.
@@ -981,6 +1098,18 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
                 return rc;
             const int C = m->layers.back().cout;
             HIP_TRY(tik::launch_merge(f, (long long)n * to * m->V, C, ld, feat + (size_t)n0 * to * m->feat, st));
+        }
+        return TIK_OK;
+    }
+    if (use_x(m)) {
+        const int chunk = std::min(N, x_chunk(m, T));
+        if ((rc = tik_model_reserve(m, chunk, T))) return rc;
+        for (int n0 = 0; n0 < N; n0 += chunk) {
+            const int n = std::min(chunk, N - n0);
+            float* f;
+            if ((rc = backbone_x(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &to, st, ptrs_of(m->ws[0])))) return rc;
+            HIP_TRY(hipMemcpyAsync(feat + (size_t)n0 * to * m->feat, f, sizeof(float) * (size_t)n * to * m->feat,
+                                   hipMemcpyDeviceToDevice, st));
         }
         return TIK_OK;
     }
@@ -1100,6 +1229,18 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
             } else if ((rc = half(xs, n, ps, st, ptrs_of(ws)))) {
                 return rc;
             }
+        }
+        return TIK_OK;
+    }
+    if (use_x(m)) {
+        const int chunk = std::min(N, x_chunk(m, T));
+        if ((rc = model_reserve_ws(m, ws, chunk, T))) return rc;
+        const WsPtrs w = ptrs_of(ws);
+        const int To = tik_model_out_frames(m, T);
+        for (int n0 = 0; n0 < N; n0 += chunk) {
+            const int n = std::min(chunk, N - n0);
+            if ((rc = backbone_x(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &to, st, w))) return rc;
+            if ((rc = head_splitk(m, f, n * to, poses + (size_t)n0 * To * m->pose_dim, w.hid, w.part, st))) return rc;
         }
         return TIK_OK;
     }

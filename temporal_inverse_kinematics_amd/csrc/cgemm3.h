@@ -108,6 +108,11 @@ hipError_t launch_gcn0(const float* x, int rows, int V, int C0, const float* bn_
                        const float* wg, int ldwg, const float* bias2, const float* amix, int mix_sparse, int Cout,
                        unsigned short* out, int ldo, float* xb4, hipStream_t st);
 
+// the same with z as fp32 rows [rows][ldo] (bf16x3 path)
+hipError_t launch_gcn0_f32(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,
+                           const float* wg, int ldwg, const float* bias2, const float* amix, int mix_sparse, int Cout,
+                           float* out, int ldo, float* xb4, hipStream_t st);
+
 // SB activations [rows][ld] -> fp32 [rows][C]
 // One whole stride-1, identity-residual ST-GCN block per workgroup
 // (stblock.hip): z = ReLU(mix(x Wg') + bias2) stays in LDS, then

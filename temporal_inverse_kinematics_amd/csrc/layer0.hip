@@ -13,12 +13,14 @@
 
 namespace tik {
 
-template <int SPARSE>
+// F32OUT: z as fp32 rows [rows][ldo] (the bf16x3 path, xgemm.hip) instead of split blocks
+template <int SPARSE, bool F32OUT = false>
 __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, int rows, int C0,
                                                    const float* __restrict__ sc, const float* __restrict__ sh,
                                                    const float* __restrict__ wg, int ldwg, const float* __restrict__ bias2,
                                                    const float* __restrict__ amix, int Cout,
-                                                   unsigned short* __restrict__ out, int ldo, float* __restrict__ xb4) {
+                                                   unsigned short* __restrict__ out, int ldo, float* __restrict__ xb4,
+                                                   float* __restrict__ outf = nullptr) {
     constexpr int VT = 17;
     const int G = Cout / 4;            // channel groups per frame
     const int FPB = 256 / G;           // frames per workgroup
@@ -76,11 +78,15 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
             }
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-        f16x4 h, l;
-        split4(z, h, l);
-        unsigned short* o = obase + (size_t)wj * ldo;
-        *reinterpret_cast<f16x4*>(o) = h;
-        *reinterpret_cast<f16x4*>(o + 32) = l;
+        if constexpr (F32OUT) {
+            *reinterpret_cast<f32x4*>(outf + ((size_t)frame * VT + wj) * ldo + co) = z;
+        } else {
+            f16x4 h, l;
+            split4(z, h, l);
+            unsigned short* o = obase + (size_t)wj * ldo;
+            *reinterpret_cast<f16x4*>(o) = h;
+            *reinterpret_cast<f16x4*>(o + 32) = l;
+        }
     }
     TIK_FENCE_END();
 }
@@ -100,6 +106,26 @@ hipError_t launch_gcn0(const float* x, int rows, int V, int C0, const float* bn_
         hipLaunchKernelGGL(gcn0_kernel<1>, grid, blk, 0, st, x, rows, C0, bn_sc, bn_sh, wg, ldwg, bias2, amix, Cout, out, ldo, xb4);
     else
         hipLaunchKernelGGL(gcn0_kernel<0>, grid, blk, 0, st, x, rows, C0, bn_sc, bn_sh, wg, ldwg, bias2, amix, Cout, out, ldo, xb4);
+    return hipGetLastError();
+}
+
+hipError_t launch_gcn0_f32(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,
+                           const float* wg, int ldwg, const float* bias2, const float* amix, int mix_sparse, int Cout,
+                           float* out, int ldo, float* xb4, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    if (V != 17 || rows % 17 || C0 < 1 || C0 > 4 || ldwg < C0 || Cout % 4 || Cout / 4 > 256 || 256 % (Cout / 4) ||
+        ldo < Cout || ldo % 4)
+        return hipErrorInvalidValue;
+    const int fpb = 256 / (Cout / 4);
+    const int nframes = rows / 17;
+    (void)hipGetLastError();
+    const dim3 grid((nframes + fpb - 1) / fpb), blk(256);
+    if (mix_sparse)
+        hipLaunchKernelGGL((gcn0_kernel<1, true>), grid, blk, 0, st, x, rows, C0, bn_sc, bn_sh, wg, ldwg, bias2, amix, Cout,
+                           nullptr, ldo, xb4, out);
+    else
+        hipLaunchKernelGGL((gcn0_kernel<0, true>), grid, blk, 0, st, x, rows, C0, bn_sc, bn_sh, wg, ldwg, bias2, amix, Cout,
+                           nullptr, ldo, xb4, out);
     return hipGetLastError();
 }
 

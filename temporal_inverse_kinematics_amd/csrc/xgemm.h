@@ -1,0 +1,70 @@
+// xgemm.h — the bf16x3 implicit-GEMM kernels of the IK forward (xgemm.hip).
+//
+// Arithmetic: every fp32 operand x = p0 + p1 + p2 (three bf16 planes, round to
+// nearest even on exact fp32 residuals: exact for normal fp32, fp32's 8-bit
+// exponent), out = sum of the six products p_i q_j with i + j <= 2 on
+// v_mfma_f32_16x16x32_bf16, fp32 accumulation (the dropped ones are <= 2^-24
+// relative each). Activations stay fp32 in HBM (4 B per element, as an fp32
+// implementation): they reach LDS by direct global->LDS DMA as fp32 rows and
+// are split in registers when each wave reads its A fragment (every wave owns
+// distinct rows, so every element is split once per K step). Weights are
+// split once on the host and packed per (column tile, K step) in exactly the
+// LDS image order, so their DMA is a linear copy.
+//
+// Contraction (same row conventions as cgemm.h): rows r = (n*tout + t')*V + w;
+// segment s, tap k reads source row (n*tin + stride*t' + k - pad)*V + w, zero
+// outside [0, tin). K step = (segment, tap, 32-channel block).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace tik {
+
+struct XSeg {
+    const float* src;     // fp32 rows [rows_in][ld]
+    int ld;               // floats per row (multiple of 4)
+    int cin;              // channels (multiple of 32)
+    int kt, stride, pad, tin;
+    long long rows_in;    // rows of src (the DMA bound: reads past it return zeros)
+};
+
+struct XArgs {
+    int M, Nc, V, tout;
+    XSeg seg[2];
+    int nseg;
+    const unsigned short* wp;   // packed weight tiles (xgemm_pack), [Nc/BN][ksteps][3][BN*32] bf16
+    int ksteps;                 // K steps of all segments
+    const float* bias;          // EPI_BIAS: [Nc]; EPI_GRAPH: [V][Nc]
+    const float* resid;         // EPI_BIAS identity residual, fp32 [M][ldr] (or null)
+    int ldr;
+    const float* rx;            // EPI_BIAS small residual conv input [M][4] fp32 (layer 0; or null)
+    int rxc;
+    const float* rw;            // its weights [Nc][rxc]
+    const float* amix;          // EPI_GRAPH [V][V], A_eff[v][w]
+    int mix_sparse;
+    float* out;                 // fp32 [M][ldo]
+    int ldo;
+    int act;
+};
+
+inline int xgemm_ksteps(const XArgs& a) {
+    int k = 0;
+    for (int s = 0; s < a.nseg; ++s) k += a.seg[s].kt * (a.seg[s].cin / 32);
+    return k;
+}
+
+// epi: EPI_BIAS (cgemm.h: bias + residual + activation) or EPI_GRAPH (graph
+// mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
+hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
+
+// Host packing of the weights of up to two segments (segment s: fp32
+// W_s[n][tap * cin_s + c], row stride ldw_s) into the tile layout above,
+// bf16x3-split, with the LDS bank swizzle applied. n >= Nc and c >= cin_s are zero.
+struct XPackSeg {
+    const float* w;
+    int ldw, kt, cin;
+};
+std::vector<unsigned short> xgemm_pack(const XPackSeg* segs, int nseg, int Nc, int bn);
+
+}  // namespace tik

@@ -91,3 +91,26 @@ def test_checkpoint_reader_is_strict(tmp_path, ik_weights):
     with pytest.raises(KeyError):   # a key the module does not have
         IKPoseTrainer.load_from_checkpoint(_lightning_ckpt(tmp_path, extra, hp))
     assert isinstance(hp, argparse.Namespace)
+
+
+def test_smplx_npz_key_mapping(tmp_path):
+    """constants_from_npz (smpl_util.py:8-19 -> smplx.SMPLX.__init__ conventions)
+    on a file in the SMPL-X model-file layout gives back the constants it was
+    written from: shapedirs[..., :10], exprdirs = shapedirs[..., 300:310],
+    posedirs (V,3,486) -> (486,3V), parents = kintree_table[0] with the root
+    -1, hand means into pose_mean[25:55], landmark tables."""
+    import test_gpu_fk as fkt
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.smplx_fk import constants_from_npz
+    c = syn.synthetic_smplx_constants(seed=5, num_verts=600, num_faces=900)
+    c["extra_verts"] = np.minimum(syn.SMPLX_EXTRA_VERTS, 599).astype(np.int32)
+    path = tmp_path / "SMPLX_MALE.npz"
+    fkt._write_smplx_npz(path, c)
+    got = constants_from_npz(str(path))
+    for k in ("v_template", "shapedirs", "exprdirs", "posedirs", "J_regressor", "lbs_weights", "lmk_faces_idx",
+              "lmk_bary_coords", "dynamic_lmk_faces_idx", "dynamic_lmk_bary_coords", "pose_mean"):
+        np.testing.assert_array_equal(got[k], c[k], err_msg=k)
+    np.testing.assert_array_equal(got["parents"], c["parents"])
+    np.testing.assert_array_equal(got["faces"], c["faces"])
+    flat = constants_from_npz(str(path), flat_hand_mean=True)
+    assert not flat["pose_mean"].any()

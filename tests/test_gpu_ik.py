@@ -13,8 +13,9 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["bf16x3", "fp32", "f16x3", "f16x3-dma", "f16x3-reg", "f16x3-dmachunk",
-                                                 "f16x3-layered", "f16x3-nofuse", "f16x3-dmahead"])
+@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
+                                                 "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
+                                                 "f16x3-dmahead"])
 def model(request):
     """bf16x3 (the default: 6-product bf16 split, fp32 range); fp32 MFMA;
     f16x3 with the default GEMM path (split-block activations with
@@ -36,7 +37,11 @@ def model(request):
         env = {"dmachunk": {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"},
                "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"},
                "nofuse": {"TIK_GEMM_PATH": "dma", "TIK_FUSE_TG": "0"},
-               "dmahead": {"TIK_GEMM_PATH": "dma", "TIK_SMALL_HEAD": "0"}}.get(path, {"TIK_GEMM_PATH": path})
+               "dmahead": {"TIK_GEMM_PATH": "dma", "TIK_SMALL_HEAD": "0"},
+               # bf16x3 on the register-staged cgemm.hip tiles instead of xgemm.hip
+               "cgemm": {"TIK_XGEMM": "0"},
+               # xgemm in sub-batches of at most 3 windows (the 2 GiB-per-tensor split)
+               "xchunk": {"TIK_DMA_CHUNK": "3"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created

@@ -53,6 +53,35 @@ __device__ __forceinline__ void xsplit8(const f32x4 lo, const f32x4 hi, xbf16x8&
 
 __device__ __forceinline__ int xa_swz(int r) { return (r >> 1) & 7; }
 
+// graph mix of one frame, output joints [W0, W1): z[w] = sum_v A[v][w] y[v] +
+// bias2[w], ReLU, stored. w and v are compile-time, so the sparse COCO
+// pattern unrolls and the A entries are wave-uniform scalar loads.
+// A_eff entry i from the 5 VGPRs that hold it across the wave (lane i % 64 of amv[i / 64])
+__device__ __forceinline__ float xam(const float (&amv)[5], int i) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[i / 64]), i % 64));
+}
+
+template <int W0, int W1, bool SPARSE>
+__device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&amv)[5],
+                                           const float* __restrict__ bias2, int Nc, int col, float* __restrict__ o,
+                                           int ldo) {
+#pragma unroll
+    for (int w = W0; w < W1; ++w) {
+        f32x4 z = *reinterpret_cast<const f32x4*>(bias2 + w * Nc + col);
+        if constexpr (SPARSE) {
+#pragma unroll
+            for (int v = 0; v < 17; ++v)
+                if ((coco_hop2_mask3(w) >> v) & 1u) z += xam(amv, v * 17 + w) * y[v];
+        } else {
+#pragma unroll
+            for (int v = 0; v < 17; ++v) z += xam(amv, v * 17 + w) * y[v];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+        *reinterpret_cast<f32x4*>(o + (size_t)w * ldo) = z;
+    }
+}
+
 template <int BN, int EPI>
 struct XCfg {
     static constexpr int NW = 8, NT = 512, BM = 256, FM = 2, FN = BN / 16;
@@ -66,7 +95,8 @@ struct XCfg {
     static constexpr int RT = EPI == EPI_GRAPH ? 255 : 256;   // valid rows per tile
     static constexpr int HB = BN / 2;                         // epilogue columns per pass
     static constexpr int LDC = HB + 4;
-    static constexpr int CT = BM * LDC * 4;
+    static constexpr int LDCG = BN + 4;                       // EPI_GRAPH: the whole tile at once
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 : BM * LDC * 4;
     static constexpr int SMEM = NST * STAGE > CT ? NST * STAGE : CT;
     static_assert(NIA * 1024 * NW == ABYTES, "A DMA split");
     static_assert(SMEM <= 160 * 1024, "LDS");
@@ -195,10 +225,48 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    // ---- epilogue: C tile through LDS, half the columns per pass
+    // ---- epilogue: C tile through LDS
     float* Cs = reinterpret_cast<float*>(smem);
     const int crow = wave * 32 + 4 * g;
     const int ccol = lane & 15;
+    if constexpr (EPI == EPI_GRAPH) {
+        __syncthreads();   // every wave done with the K loop's LDS
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Cs[(crow + i * 16 + e) * C::LDCG + j * 16 + ccol] = acc[i][j][e];
+        // A_eff in 5 VGPRs across the wave, read back with v_readlane (global loads
+        // would be re-issued after every store, which may alias them)
+        float amv[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) amv[k] = 64 * k + lane < 17 * 17 ? a.amix[64 * k + lane] : 0.f;
+        __syncthreads();
+        // waves 0-3 produce joints 0-8, waves 4-7 joints 9-16 (wave-uniform split,
+        // so each half's joint loop is compile-time); item = (frame, 4 columns)
+        constexpr int C4 = BN / 4;
+        const int nframes = a.M / 17, f0 = r0 / 17;
+        const bool second = wave >= NW / 2;
+#pragma unroll 1
+        for (int it = tid & (NT / 2 - 1); it < 15 * C4; it += NT / 2) {
+            const int f = it / C4, c4 = it - f * C4;
+            const int col = n0 + 4 * c4;
+            if (f0 + f >= nframes || col >= a.Nc) continue;
+            f32x4 y[17];
+#pragma unroll
+            for (int v = 0; v < 17; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * 17 + v) * C::LDCG + 4 * c4);
+            float* o = a.out + (size_t)(f0 + f) * 17 * a.ldo + col;
+            if (a.mix_sparse) {
+                if (second) xmix_store<9, 17, true>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+                else xmix_store<0, 9, true>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+            } else {
+                if (second) xmix_store<9, 17, false>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+                else xmix_store<0, 9, false>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+            }
+        }
+        return;
+    }
     const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -212,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
                     Cs[(crow + i * 16 + e) * C::LDC + jj * 16 + ccol] = acc[i][half * (FN / 2) + jj][e];
         __syncthreads();
         const int cbase = n0 + half * C::HB;
-        if constexpr (EPI == EPI_BIAS) {
+        {
             // KI items per thread, all global operands loaded before any store
             constexpr int C4 = C::HB / 4, KI = C::BM * C4 / NT;
             static_assert(KI * NT == C::BM * C4, "epilogue mapping");
@@ -260,41 +328,6 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
                         t = t > 0.f ? t : slope * t;
                         a.out[(size_t)row * a.ldo + col + e] = t;
                     }
-                }
-            }
-        } else {
-            // item = (frame f of 15, 4-column group c4, joint half wh): z for joints [9wh, 9wh+9)
-            constexpr int C4 = C::HB / 4;
-            const int nframes = a.M / 17, f0 = r0 / 17;
-            for (int it = tid; it < 15 * C4 * 2; it += NT) {
-                const int wh = it & 1, rest = it >> 1;
-                const int f = rest / C4, c4 = rest - f * C4;
-                const int col = cbase + 4 * c4;
-                if (f0 + f >= nframes || col >= a.Nc) continue;
-                f32x4 y[17];
-#pragma unroll
-                for (int v = 0; v < 17; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * 17 + v) * C::LDC + 4 * c4);
-                float* o = a.out + (size_t)(f0 + f) * 17 * a.ldo + col;
-                f32x4 b2[9];
-#pragma unroll
-                for (int ww = 0; ww < 9; ++ww)
-                    b2[ww] = *reinterpret_cast<const f32x4*>(a.bias + min(wh * 9 + ww, 16) * a.Nc + col);
-#pragma unroll
-                for (int ww = 0; ww < 9; ++ww) {
-                    const int w = wh * 9 + ww;
-                    if (w >= 17) break;
-                    f32x4 z = b2[ww];
-                    if (a.mix_sparse) {
-#pragma unroll
-                        for (int v = 0; v < 17; ++v)
-                            if ((coco_hop2_mask3(w) >> v) & 1u) z += a.amix[v * 17 + w] * y[v];
-                    } else {
-#pragma unroll
-                        for (int v = 0; v < 17; ++v) z += a.amix[v * 17 + w] * y[v];
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-                    *reinterpret_cast<f32x4*>(o + (size_t)w * a.ldo) = z;
                 }
             }
         }

@@ -136,6 +136,16 @@ int tik_window_gather(const float* seq, int F, int V, int idx0, int n_idx, int h
                       int root_b, int relative, float* windows, void* stream);
 
 /* ------------------------------------------------------------------------
+ * moveai_3d -> COCO-17 keypoints on the device (inference.py:121-133 with
+ * common/keypoints_util.py:27-60 generate_moveai3d_to_coco_mappings /
+ * convert_seq_keypoints): out[f][c] = joints[f][map17[c]] (map17: 17 host ints,
+ * -1 = none), COCO 0 = 0.5 (joints[f][J-1] + joints[f][J-2]) (nose = mid of
+ * the ears), 1 = joints[f][J-2], 2 = joints[f][J-1] (eyes = ears), then
+ * (x, y, z) -> (x, z, -y). joints (F,J,3), out (F,17,3), device fp32.
+ * ---------------------------------------------------------------------- */
+int tik_moveai_to_coco(const float* joints, int F, int J, const int* map17_host, float* out, void* stream);
+
+/* ------------------------------------------------------------------------
  * Online IK (BASELINE.json config #5): stride-1 sliding window over a live
  * sequence. tik_stream_push copies one frame (V=17 x 3 host floats) into a
  * device ring, gathers the window centred h = win_size/2 frames back (left

@@ -54,6 +54,7 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_gconv_fwd": (_I, (_P, _I, _I, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P)),
     "tik_aa_to_rotmat": (_I, (_P, _I, _P, _P)),
     "tik_window_gather": (_I, (_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P)),
+    "tik_moveai_to_coco": (_I, (_P, _I, _I, ctypes.POINTER(ctypes.c_int), _P, _P)),
     "tik_stream_create": (_I, (_P, _I, _I, ctypes.POINTER(_P))),
     "tik_stream_destroy": (_I, (_P,)),
     "tik_stream_reset": (_I, (_P,)),

@@ -98,6 +98,42 @@ int drain_mask() {
     return m;
 }
 
+// debug (TIK_X_TRACE=1): launch an xgemm with per-workgroup phase stamps and
+// print the averages (s_memtime cycles) to stderr; synchronizes the stream
+hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, const char* label) {
+    static const bool on = getenv("TIK_X_TRACE") != nullptr;
+    if (!on) return tik::launch_xgemm(a, bn, epi, st);
+    const int rt = epi == tik::EPI_GRAPH ? 255 : 256;
+    const long long nwg = (long long)((a.M + rt - 1) / rt) * ((a.Nc + bn - 1) / bn);
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc(&d, nwg * 8 * 8);
+    if (e != hipSuccess) return e;
+    (void)hipMemset(d, 0, nwg * 8 * 8);
+    a.trace = d;
+    e = tik::launch_xgemm(a, bn, epi, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<unsigned long long> h(nwg * 8);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    double s[6] = {0, 0, 0, 0, 0, 0}, n = 0, ks = 0;
+    for (long long w = 0; w < nwg; ++w) {
+        if (!h[8 * w + 7]) continue;
+        n += 1; ks = (double)h[8 * w + 6];
+        for (int k = 0; k < 6; ++k) s[k] += (double)h[8 * w + k];
+    }
+    n = std::max(1.0, n);
+    fprintf(stderr, "XTRACE %-10s wg %6.0f ksteps %3.0f | cycles/wg: prologue %7.0f main %8.0f iden %6.0f epi %7.0f | "
+            "barrier %7.0f vmwait %7.0f | main/kstep %6.0f\n", label, n, ks, s[0] / n, s[1] / n, s[2] / n, s[3] / n,
+            s[4] / n, s[5] / n, s[1] / n / std::max(1.0, ks));
+    return e;
+}
+
+// tuning experiments on the xgemm kernels (XArgs::tune), TIK_XTUNE=<bits>; 0 in production
+int xtune() {
+    static const int t = getenv("TIK_XTUNE") ? atoi(getenv("TIK_XTUNE")) : 0;
+    return t;
+}
+
 // Optional per-launch HIP-event profiler (bench.py's roofline numbers): one
 // event pair per kernel launch on the launch stream, algorithmic FLOPs and
 // bytes computed from the shapes.
@@ -356,11 +392,12 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
+            g.tune = xtune();
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
             p.out(z, (size_t)rin * cout * 4);
-            HIP_TRY(tik::launch_xgemm(g, xg_bn, tik::EPI_GRAPH, st));
+            HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
         tik::XArgs t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
@@ -375,16 +412,17 @@ struct Layer {
             t.nseg = 2;
             fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout);
         } else if (res == RES_IDEN) {
-            t.resid = x; t.ldr = ld;
+            t.idn = tik::XSeg{x, ld, cin, 1, 1, 0, to, rin};
             by += 4.0 * px_out * cout;
         }
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
-        if (t.ksteps != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, t.ksteps, xt_ks);
+        if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
+        t.tune = xtune();
         const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
-        HIP_TRY(tik::launch_xgemm(t, xt_bn, tik::EPI_BIAS, st));
+        HIP_TRY(launch_xgemm_traced(t, xt_bn, tik::EPI_BIAS, st, lab.c_str()));
         return TIK_OK;
     }
 
@@ -1358,6 +1396,15 @@ int tik_gconv_fwd(const float* x, int N, int Cin, int T, int V, const float* A, 
 int tik_aa_to_rotmat(const float* aa, int n, float* R, void* stream) {
     if (!aa || !R || n < 0) return fail(TIK_E_INVALID, "tik_aa_to_rotmat: bad arguments");
     HIP_TRY(tik::launch_aa_to_rotmat(aa, n, R, (hipStream_t)stream));
+    return TIK_OK;
+}
+
+int tik_moveai_to_coco(const float* joints, int F, int J, const int* map17_host, float* out, void* stream) {
+    if (!joints || !map17_host || !out || F < 0 || J < 2) return fail(TIK_E_INVALID, "tik_moveai_to_coco: bad arguments");
+    for (int c = 0; c < 17; ++c)
+        if (map17_host[c] < -1 || map17_host[c] >= J)
+            return fail(TIK_E_INVALID, "tik_moveai_to_coco: map entry %d = %d out of range for %d joints", c, map17_host[c], J);
+    HIP_TRY(tik::launch_moveai_to_coco(joints, F, J, map17_host, out, (hipStream_t)stream));
     return TIK_OK;
 }
 

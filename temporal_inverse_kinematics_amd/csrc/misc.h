@@ -12,6 +12,11 @@ hipError_t launch_gconv(const float* x, int N, int Cin, int T, int V, const floa
                         const float* W, const float* b, int Cout, int tk, int ts, int tp, int td,
                         int To, float* out, hipStream_t st);
 
+// moveai_3d -> COCO-17 (inference.py:121-133): gather by map (17 entries, -1 = none),
+// COCO 0 = mid of the last two joints (the ears), 1 / 2 = the last-but-one / last
+// joint, then (x, y, z) -> (x, z, -y). joints (F,J,3) -> out (F,17,3)
+hipError_t launch_moveai_to_coco(const float* joints, int F, int J, const int* map17, float* out, hipStream_t st);
+
 hipError_t launch_pad_channels(const float* x, long long rows, int C, int Cp, float* y, hipStream_t st);
 
 hipError_t launch_stream_push(float* ring, int W, int nv, int* count, const float* frame, hipStream_t st);

@@ -231,4 +231,45 @@ hipError_t launch_checksum(const void* p, size_t bytes, unsigned long long* out,
     return hipGetLastError();
 }
 
+struct Map17 {
+    int m[17];
+};
+
+// one thread per (frame, COCO joint): a pure gather + the axis swap, so the
+// output is bit-identical to the reference's numpy (0.5 * (a + b) in fp32 is an
+// exact halving of the fp32 sum, as numpy computes it on float32 arrays)
+__global__ void moveai_to_coco_kernel(const float* __restrict__ j, int F, int J, Map17 mp, float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)F * 17) return;
+    const int c = (int)(i % 17);
+    const long long f = i / 17;
+    const float* jf = j + f * J * 3;
+    float x = 0.f, y = 0.f, z = 0.f;
+    if (c == 0) {
+        x = 0.5f * (jf[(J - 1) * 3 + 0] + jf[(J - 2) * 3 + 0]);
+        y = 0.5f * (jf[(J - 1) * 3 + 1] + jf[(J - 2) * 3 + 1]);
+        z = 0.5f * (jf[(J - 1) * 3 + 2] + jf[(J - 2) * 3 + 2]);
+    } else {
+        const int src = c == 1 ? J - 2 : (c == 2 ? J - 1 : mp.m[c]);
+        if (src >= 0) { x = jf[src * 3]; y = jf[src * 3 + 1]; z = jf[src * 3 + 2]; }
+    }
+    float* o = out + i * 3;
+    o[0] = x;
+    o[1] = z;
+    o[2] = -y;
+}
+
+hipError_t launch_moveai_to_coco(const float* joints, int F, int J, const int* map17, float* out, hipStream_t st) {
+    if (F <= 0) return hipSuccess;
+    Map17 mp;
+    for (int c = 0; c < 17; ++c) {
+        if (map17[c] >= J) return hipErrorInvalidValue;
+        mp.m[c] = map17[c];
+    }
+    const long long n = (long long)F * 17;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(moveai_to_coco_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, joints, F, J, mp, out);
+    return hipGetLastError();
+}
+
 }  // namespace tik

@@ -74,6 +74,7 @@ struct tik_trainer {
     DevBuf P, G, M, Vv, B;
     long long np = 0, nb = 0;
     long long dg = -1, db = -1, rm0 = -1, rv0 = -1, A = -1;       // data_bn + adjacency
+    bool zero_pending = false;                                     // gA/gB reallocated: zero them on the step's stream
     long long w1 = -1, b1 = -1, w2 = -1, b2 = -1;                  // head
     int feat = 0, pose_dim = 0;
     DevBuf w1b, w2b;                                               // W1^T [feat][512], W2^T [512][ldp]
@@ -188,9 +189,10 @@ int reserve(tik_trainer* t, int N, int T) {
         (rc = t->tH.reserve(big)) || (rc = t->tZ.reserve(big)) || (rc = t->tY.reserve(big)) ||
         (rc = t->col.reserve(colsz)) || (rc = t->up.reserve(big)))
         return rc;
-    // layer 0's input gradient has 3 of 4 columns written: keep the padding column zero
-    HIP_TRY(hipMemset(t->gA.p, 0, big * sizeof(float)));
-    HIP_TRY(hipMemset(t->gB.p, 0, big * sizeof(float)));
+    // the gradient ping-pong buffers start zeroed (stream-ordered, in step()); their
+    // padding column (layer 0's 4th input channel) is never read: bn_bwd_finalize
+    // zeroes it through cmap0 = -1
+    t->zero_pending = true;
     t->N = N;
     t->T = T;
     return TIK_OK;
@@ -384,6 +386,11 @@ int step(tik_trainer* t, const float* x, int N, int T, const float* target, cons
          unsigned long long seed, float* loss_out, hipStream_t st) {
     int rc;
     if ((rc = reserve(t, N, T))) return rc;
+    if (t->zero_pending) {
+        HIP_TRY(hipMemsetAsync(t->gA.p, 0, t->gA.n * sizeof(float), st));
+        HIP_TRY(hipMemsetAsync(t->gB.p, 0, t->gB.n * sizeof(float), st));
+        t->zero_pending = false;
+    }
     (void)hipGetLastError();
     const long long R0 = (long long)N * T, p0 = R0 * V;
     float* P = t->P.p;
@@ -602,9 +609,11 @@ int tik_trainer_destroy(tik_trainer_t t) {
 int tik_trainer_step(tik_trainer_t t, const float* x, int N, int T, const float* target, const float* dropout_mask,
                      unsigned long long seed, float* loss, void* stream) {
     if (!t || !x || !target || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_trainer_step: bad arguments");
-    int tt = T;
-    for (const TLayer& l : t->L) tt = (tt - 1) / l.stride + 1;
-    if ((long long)N * T * V * 4 > (1LL << 31) - 1)
+    // every float4 launcher indexes rows x channels / 4 in 32 bits: check the widest
+    // activation up front, before any kernel updates running statistics
+    int maxc = 4;
+    for (const TLayer& l : t->L) maxc = std::max(maxc, std::max(l.cinp, l.cout));
+    if ((long long)N * T * V * maxc / 4 > (1LL << 31) - 1 || (long long)N * T * V * 4 > (1LL << 31) - 1)
         return fail(TIK_E_INVALID, "tik_trainer_step: batch of %d x %d frames too large", N, T);
     if (N * T < 2) return fail(TIK_E_INVALID, "tik_trainer_step: BatchNorm needs more than one value per channel");
     hipStream_t st = (hipStream_t)stream;

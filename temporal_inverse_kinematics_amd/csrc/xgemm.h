@@ -33,11 +33,15 @@ struct XArgs {
     int M, Nc, V, tout;
     XSeg seg[2];
     int nseg;
-    const unsigned short* wp;   // packed weight tiles (xgemm_pack), [Nc/BN][ksteps][3][BN*32] bf16
-    int ksteps;                 // K steps of all segments
+    const unsigned short* wp;   // packed weight tiles (xgemm_pack), [Nc/BN][kmain][3][BN*32] bf16
+    int ksteps;                 // K steps of all segments (xgemm_ksteps)
+    // identity residual (EPI_BIAS): idn.src = the block input rows, read at the
+    // output row (kt 1, stride 1, pad 0); null = none. Added inside the K loop
+    // as idn.cin/32 extra K steps against the identity (x = p0 + p1 + p2, three
+    // MFMAs with a constant 1.0 operand: an exact add), so its rows stream
+    // through the DMA ring with the other operands instead of the epilogue
+    XSeg idn;
     const float* bias;          // EPI_BIAS: [Nc]; EPI_GRAPH: [V][Nc]
-    const float* resid;         // EPI_BIAS identity residual, fp32 [M][ldr] (or null)
-    int ldr;
     const float* rx;            // EPI_BIAS small residual conv input [M][4] fp32 (layer 0; or null)
     int rxc;
     const float* rw;            // its weights [Nc][rxc]
@@ -46,13 +50,17 @@ struct XArgs {
     float* out;                 // fp32 [M][ldo]
     int ldo;
     int act;
+    int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA
+    unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null
 };
 
-inline int xgemm_ksteps(const XArgs& a) {
+// K steps with packed weight tiles (the segments), and all K steps (+ identity)
+__host__ __device__ inline int xgemm_kmain(const XArgs& a) {
     int k = 0;
     for (int s = 0; s < a.nseg; ++s) k += a.seg[s].kt * (a.seg[s].cin / 32);
     return k;
 }
+__host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain(a) + (a.idn.src ? a.idn.cin / 32 : 0); }
 
 // epi: EPI_BIAS (cgemm.h: bias + residual + activation) or EPI_GRAPH (graph
 // mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile

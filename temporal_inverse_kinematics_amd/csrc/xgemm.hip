@@ -85,19 +85,22 @@ __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&a
 template <int BN, int EPI>
 struct XCfg {
     static constexpr int NW = 8, NT = 512, BM = 256, FM = 2, FN = BN / 16;
+    static constexpr bool TR = EPI == EPI_BIAS;   // transposed MFMA: each lane ends with 4 channels of a row
     static constexpr int ABYTES = BM * 128;
     static constexpr int PLANE = BN * 64;
     static constexpr int BBYTES = 3 * PLANE;
-    static constexpr int STAGE = ABYTES + BBYTES;
-    static constexpr int NST = BN >= 128 ? 2 : 3;
+    // A rows are DMA'd and consumed by the same wave (wave w fills and reads rows
+    // 32w..32w+31), so the A ring needs no barrier: 2 slots, issued 2 steps ahead
+    // (a slot is free once its step's fragments were split, one step early).
+    // B (weights) is shared by all waves: 3 slots, issued 2 steps ahead, one barrier per step.
+    static constexpr int NSA = 2, NSB = 3;
+    static constexpr int RING = NSA * ABYTES + NSB * BBYTES;
     static constexpr int NIA = ABYTES / 1024 / NW;   // A DMA instructions per wave per stage
     static constexpr int NIB_TOT = BBYTES / 1024;
     static constexpr int RT = EPI == EPI_GRAPH ? 255 : 256;   // valid rows per tile
-    static constexpr int HB = BN / 2;                         // epilogue columns per pass
-    static constexpr int LDC = HB + 4;
-    static constexpr int LDCG = BN + 4;                       // EPI_GRAPH: the whole tile at once
-    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 : BM * LDC * 4;
-    static constexpr int SMEM = NST * STAGE > CT ? NST * STAGE : CT;
+    static constexpr int LDCG = BN + 4;
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 : 0;
+    static constexpr int SMEM = RING > CT ? RING : CT;
     static_assert(NIA * 1024 * NW == ABYTES, "A DMA split");
     static_assert(SMEM <= 160 * 1024, "LDS");
 };
@@ -105,11 +108,15 @@ struct XCfg {
 template <int BN, int EPI>
 __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     using C = XCfg<BN, EPI>;
-    constexpr int NW = C::NW, NT = C::NT, FM = C::FM, FN = C::FN, NIA = C::NIA, NST = C::NST, RT = C::RT;
+    constexpr int NW = C::NW, NT = C::NT, FM = C::FM, FN = C::FN, NIA = C::NIA, NSA = C::NSA, NSB = C::NSB,
+                  RT = C::RT;
+    constexpr bool TR = C::TR;
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];   // the only LDS object
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool tr = a.trace != nullptr;
+    unsigned long long t0 = tr ? __builtin_amdgcn_s_memtime() : 0, t_bar = 0, t_vm = 0, t1 = 0, t2 = 0, t3 = 0;
     int r0, ntile;
     {   // XCD-aware tile order: consecutive workgroup ids go to different XCDs,
         // so give each XCD a contiguous run of tiles (rows shared by neighbours stay in its L2)
@@ -123,6 +130,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     const int V = a.V;
 
     // ---- A DMA roles: instruction j of this wave fills rows (wave*NIA + j)*8 + lane/8, unit lane&7
+    // (with NIA = 4 those are rows 32 wave .. 32 wave + 31: exactly the rows this wave computes)
     int a_n[NIA], a_t[NIA], a_w[NIA], a_uo[NIA];
     bool a_ok[NIA];
 #pragma unroll
@@ -137,42 +145,57 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
         a_n[j] = q / a.tout;
         a_t[j] = q - a_n[j] * a.tout;
     }
-    // B DMA: the stage's B image is one contiguous packed block; instruction q (of NIB_TOT) copies 1 KB
-    const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * a.ksteps * C::BBYTES));
-    const int nb_w = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage
-    const int nper = NIA + nb_w;
+    const int kmain = xgemm_kmain(a);   // K steps with weight tiles; the identity steps follow
+    const int K = a.ksteps;
+    // B DMA: a stage's B image is one contiguous packed block; instruction q (of NIB_TOT) copies 1 KB
+    const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kmain * C::BBYTES));
+    const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage
 
+    // A and B cursors over (segment, tap, 32-channel block); segment a.nseg is the identity residual
     struct Cur { int seg, tap, blk, k; };
-    Cur cur{0, 0, 0, 0};
+    auto segof = [&](int sgi) -> XSeg { return sgi == 0 ? a.seg[0] : (sgi == 1 && a.nseg > 1 ? a.seg[1] : a.idn); };
+    auto advance = [&](Cur& c) {
+        const XSeg sg = segof(c.seg);
+        ++c.k;
+        if (++c.blk >= sg.cin / 32) { c.blk = 0; if (++c.tap >= sg.kt) { c.tap = 0; ++c.seg; } }
+    };
+    Cur ca{0, 0, 0, 0}, cb{0, 0, 0, 0};
     unsigned a_off[NIA];
     i32x4 rA = buf_rsrc(a.seg[0].src, (unsigned)(a.seg[0].rows_in * a.seg[0].ld * 4));
     int cached_seg = -1, cached_tap = -1;
     auto prepare = [&]() {
-        if (cur.seg == cached_seg && cur.tap == cached_tap) return;
-        const XSeg sg = cur.seg == 0 ? a.seg[0] : a.seg[1];
-        if (cur.seg != cached_seg) rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
+        if (ca.seg == cached_seg && ca.tap == cached_tap) return;
+        const XSeg sg = segof(ca.seg);
+        if (ca.seg != cached_seg) rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
 #pragma unroll
         for (int j = 0; j < NIA; ++j) {
-            const int t = sg.stride * a_t[j] + cur.tap - sg.pad;
+            const int t = sg.stride * a_t[j] + ca.tap - sg.pad;
             a_off[j] = (a_ok[j] && t >= 0 && t < sg.tin)
                            ? (unsigned)(((a_n[j] * sg.tin + t) * V + a_w[j]) * sg.ld * 4 + a_uo[j])
                            : DMA_OOB;
         }
-        cached_seg = cur.seg; cached_tap = cur.tap;
+        cached_seg = ca.seg; cached_tap = ca.tap;
     };
-    auto issue = [&](int slot) {   // stage of the cursor, then advance it
+    auto a_slot = [&](int s) { return smem + s * C::ABYTES; };
+    auto b_slot = [&](int s) { return smem + NSA * C::ABYTES + s * C::BBYTES; };
+    auto issue_a = [&]() {   // the A cursor's step, into its ring slot
         prepare();
-        unsigned char* A = smem + slot * C::STAGE;
-        const int soA = __builtin_amdgcn_readfirstlane(cur.blk * 128);
+        unsigned char* A = a_slot(ca.k % NSA);
+        const int soA = __builtin_amdgcn_readfirstlane(ca.blk * 128);
+        if (!(a.tune & 1))
 #pragma unroll
-        for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
-        const int soB = __builtin_amdgcn_readfirstlane((ntile * a.ksteps + cur.k) * C::BBYTES);
-        for (int q = wave; q < C::NIB_TOT; q += NW) dma16(rB, A + C::ABYTES + q * 1024, (unsigned)(q * 1024 + lane * 16), soB);
-        const int nb = (cur.seg == 0 ? a.seg[0].cin : a.seg[1].cin) / 32;
-        const int kt = cur.seg == 0 ? a.seg[0].kt : a.seg[1].kt;
-        ++cur.k;
-        if (++cur.blk >= nb) { cur.blk = 0; if (++cur.tap >= kt) { cur.tap = 0; ++cur.seg; } }
+            for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
+        advance(ca);
     };
+    auto issue_b = [&]() {   // the B cursor's step (main steps only)
+        unsigned char* B = b_slot(cb.k % NSB);
+        const int soB = __builtin_amdgcn_readfirstlane((ntile * kmain + cb.k) * C::BBYTES);
+        if (!(a.tune & 2))
+            for (int q = wave; q < C::NIB_TOT; q += NW) dma16(rB, B + q * 1024, (unsigned)(q * 1024 + lane * 16), soB);
+        advance(cb);
+    };
+    // VMEM instructions this wave issues for step k (vmcnt accounting)
+    auto n_issued = [&](int k) { return k >= K ? 0 : NIA + (k < kmain ? nbw : 0); };
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -182,54 +205,195 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     const int g = lane >> 4;
     const int bsw = (-((lane & 15) >> 2)) & 3;
     const int boff = (lane & 15) * 64 + ((g ^ bsw) << 4);
-    auto compute = [&](int slot) {
-        const unsigned char* A = smem + slot * C::STAGE;
-        const unsigned char* B = A + C::ABYTES;
-        xbf16x8 a0[FM], a1[FM], a2[FM];
+    auto mma = [&](const xbf16x8& x, const xbf16x8& w, f32x4& c) {
+        // TR: C^T = W . X^T, so lane l holds row (l & 15), channels 4(l >> 4) .. +3
+        c = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0)
+               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, w, c, 0, 0, 0);
+    };
+    // this wave's A fragments of a step: fp32 rows -> three bf16 planes
+    auto read_a = [&](int k, f32x4 (&lo)[FM], f32x4 (&hi)[FM]) {
+        const unsigned char* A = a_slot(k % NSA);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
             const int r = wave * 32 + i * 16 + (lane & 15);
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(A + r * 128 + ((g ^ xa_swz(r)) << 4));
-            const f32x4 hi = *reinterpret_cast<const f32x4*>(A + r * 128 + (((g + 4) ^ xa_swz(r)) << 4));
-            xsplit8(lo, hi, a0[i], a1[i], a2[i]);
+            lo[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + ((g ^ xa_swz(r)) << 4));
+            hi[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + (((g + 4) ^ xa_swz(r)) << 4));
         }
+    };
+    xbf16x8 c0[FM], c1[FM], c2[FM];   // the current step's split A
+    f32x4 alo[FM], ahi[FM];
+
+    // ---- main steps: the split of step k+1 runs under step k's MFMAs
+    // issue order: B(0) A(0) B(1) A(1) | per step k: B(k+2) A(k+2), so a wait
+    // for this wave's A(k) (in issue order) also retires its B(k)
+    if (kmain > 0) issue_b();
+    issue_a();
+    if (1 < kmain) issue_b();
+    if (1 < K) issue_a();
+    wait_vm_dyn(n_issued(1));   // A(0) (and B(0)) landed
+    if (tr) t1 = __builtin_amdgcn_s_memtime();
+    if (kmain > 0) {
+        read_a(0, alo, ahi);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) xsplit8(alo[i], ahi[i], c0[i], c1[i], c2[i]);
+    }
+    // one main step: MFMAs of step k on the split held in cur, with step k+1's A
+    // reads and split into nxt interleaved between them (the loop below runs it
+    // twice per iteration with the two register sets swapped: no copies)
+    xbf16x8 d0[FM], d1[FM], d2[FM];
+    auto main_step = [&](int k, xbf16x8 (&u0)[FM], xbf16x8 (&u1)[FM], xbf16x8 (&u2)[FM], xbf16x8 (&v0)[FM],
+                         xbf16x8 (&v1)[FM], xbf16x8 (&v2)[FM]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long tb0 = tr ? __builtin_amdgcn_s_memtime() : 0;
+        __builtin_amdgcn_s_barrier();   // every wave's B(k) landed; every wave done reading B(k-1)
+        if (tr) t_bar += __builtin_amdgcn_s_memtime() - tb0;
+        if (k + 2 < kmain) issue_b();
+        if (k + 2 < K) issue_a();
+        // this wave's A(k+1) landed (B(k+2), A(k+2) may still fly); past the last
+        // step the read + split below run on a stale slot and are discarded
+        {
+            const unsigned long long tv0 = tr ? __builtin_amdgcn_s_memtime() : 0;
+            wait_vm_dyn(n_issued(k + 2));
+            if (tr) t_vm += __builtin_amdgcn_s_memtime() - tv0;
+        }
+        const unsigned char* B = b_slot(k % NSB) + boff;
+        // one scheduling region: step k's MFMAs with step k+1's A reads and split
+        // and step k's B reads interleaved between them (sched_group_barrier below)
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(k + 1, alo, ahi);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-            const xbf16x8 b0 = *reinterpret_cast<const xbf16x8*>(B + j * 16 * 64 + boff);
-            const xbf16x8 b1 = *reinterpret_cast<const xbf16x8*>(B + C::PLANE + j * 16 * 64 + boff);
-            const xbf16x8 b2 = *reinterpret_cast<const xbf16x8*>(B + 2 * C::PLANE + j * 16 * 64 + boff);
+            xbf16x8 b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE + j * 16 * 64);
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b0, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b2, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b0, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b1, acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0, acc[i][j], 0, 0, 0);
+                mma(u2[i], b[0], acc[i][j]);
+                mma(u1[i], b[1], acc[i][j]);
+                mma(u0[i], b[2], acc[i][j]);
+                mma(u1[i], b[0], acc[i][j]);
+                mma(u0[i], b[1], acc[i][j]);
+                mma(u0[i], b[0], acc[i][j]);
             }
+            if (j == 0)
+#pragma unroll
+                for (int i = 0; i < FM; ++i) xsplit8(alo[i], ahi[i], v0[i], v1[i], v2[i]);
+        }
+        // pattern: the A reads and the first B block's reads, then per MFMA up to two
+        // VALU and, every third MFMA, one LDS read
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * FM + 3, 0);
+#pragma unroll
+        for (int q = 0; q < 6 * FM * FN; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (q % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int k = 0; k < kmain; k += 2) {
+        main_step(k, c0, c1, c2, d0, d1, d2);
+        if (k + 1 < kmain) main_step(k + 1, d0, d1, d2, c0, c1, c2);
+    }
+    if (tr) t2 = __builtin_amdgcn_s_memtime();
+    // ---- identity residual steps (TR): acc += x, exact fp32 adds from this wave's rows
+    if constexpr (TR) {
+        for (int k = kmain; k < K; ++k) {
+            wait_vm_dyn(k + 1 < K ? NIA : 0);   // A(k) landed (only A(k+1) was issued after it)
+            const unsigned char* A = a_slot(k % NSA);
+            const int blk = k - kmain;
+            const int jb = (32 * blk - n0) / 16;   // first local column block of these channels
+            f32x4 xv[FM][2];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int r = wave * 32 + i * 16 + (lane & 15);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    // channels 32 blk + 16h + 4g .. +3 = logical floats [8 g' + 4 h', +4)
+                    const int gp = 2 * h + (g >> 1), hp = g & 1;
+                    xv[i][h] = *reinterpret_cast<const f32x4*>(A + r * 128 + (((gp + 4 * hp) ^ xa_swz(r)) << 4));
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (k + 2 < K) issue_a();   // into the slot just read
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int h = j - jb;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+                    if (h == 0) acc[i][j] += xv[i][0];
+                    else if (h == 1) acc[i][j] += xv[i][1];
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tr) t3 = __builtin_amdgcn_s_memtime();
+    auto trace_out = [&]() {
+        if (tr && tid == 0) {
+            unsigned long long* o = a.trace + 8 * (size_t)(blockIdx.y * gridDim.x + blockIdx.x);
+            o[0] = t1 - t0; o[1] = t2 - t1; o[2] = t3 - t2; o[3] = __builtin_amdgcn_s_memtime() - t3;
+            o[4] = t_bar; o[5] = t_vm; o[6] = kmain; o[7] = 1;
         }
     };
 
-    const int K = a.ksteps;
+    if constexpr (TR) {
+        // ---- EPI_BIAS from registers: acc[i][j] lane l = row wave*32 + 16i + (l & 15),
+        // channels n0 + 16j + 4(l >> 4) .. +3: float4 operands and stores, no LDS
+        const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
+        int rows[FM];
+        bool rok[FM];
 #pragma unroll
-    for (int s = 0; s < NST - 1; ++s)
-        if (s < K) issue(s);
-    for (int k = 0; k < K; ++k) {
-        // in flight: stages k .. k+younger; retire stage k (vmcnt retires in issue order)
-        const int younger = min(NST - 2, K - 1 - k);
-        wait_vm_dyn(younger * nper);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();   // every wave's stage-k DMA landed; every wave done with stage k-1
-        if (k + NST - 1 < K) issue((k + NST - 1) % NST);
-        compute(k % NST);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // ---- epilogue: C tile through LDS
-    float* Cs = reinterpret_cast<float*>(smem);
-    const int crow = wave * 32 + 4 * g;
-    const int ccol = lane & 15;
-    if constexpr (EPI == EPI_GRAPH) {
+        for (int i = 0; i < FM; ++i) {
+            const int lr = wave * 32 + i * 16 + (lane & 15);
+            rok[i] = lr < RT && r0 + lr < a.M;
+            rows[i] = rok[i] ? r0 + lr : 0;
+        }
+        f32x4 xr[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (a.rx) xr[i] = *reinterpret_cast<const f32x4*>(a.rx + (size_t)rows[i] * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + 16 * j + 4 * g;
+            if (col >= a.Nc) continue;
+            if (col + 3 < a.Nc) {
+                const f32x4 bv = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+                float rw[4][4] = {};
+                if (a.rx)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) rw[e][c] = c < a.rxc ? a.rw[(col + e) * a.rxc + c] : 0.f;
+#pragma unroll
+                for (int i = 0; i < FM; ++i) {
+                    f32x4 v = acc[i][j] + bv;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] += xr[i][0] * rw[e][0] + xr[i][1] * rw[e][1] + xr[i][2] * rw[e][2] + xr[i][3] * rw[e][3];
+                        v[e] = v[e] > 0.f ? v[e] : slope * v[e];
+                    }
+                    if (rok[i]) *reinterpret_cast<f32x4*>(a.out + (size_t)rows[i] * a.ldo + col) = v;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < FM; ++i) {
+                    if (!rok[i]) continue;
+                    for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                        float t = acc[i][j][e] + (a.bias ? a.bias[col + e] : 0.f);
+                        if (a.rx)
+                            for (int c = 0; c < a.rxc; ++c) t = fmaf(xr[i][c], a.rw[(col + e) * a.rxc + c], t);
+                        t = t > 0.f ? t : slope * t;
+                        a.out[(size_t)rows[i] * a.ldo + col + e] = t;
+                    }
+                }
+            }
+        }
+    } else {
+        // ---- EPI_GRAPH: the C tile through LDS, then the graph mix per frame
+        float* Cs = reinterpret_cast<float*>(smem);
+        const int crow = wave * 32 + 4 * g;
+        const int ccol = lane & 15;
         __syncthreads();   // every wave done with the K loop's LDS
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -265,73 +429,8 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
                 else xmix_store<0, 9, false>(y, amv, a.bias, a.Nc, col, o, a.ldo);
             }
         }
-        return;
     }
-    const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        __syncthreads();   // K loop done (first pass) / previous pass's reads done
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int jj = 0; jj < FN / 2; ++jj)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    Cs[(crow + i * 16 + e) * C::LDC + jj * 16 + ccol] = acc[i][half * (FN / 2) + jj][e];
-        __syncthreads();
-        const int cbase = n0 + half * C::HB;
-        {
-            // KI items per thread, all global operands loaded before any store
-            constexpr int C4 = C::HB / 4, KI = C::BM * C4 / NT;
-            static_assert(KI * NT == C::BM * C4, "epilogue mapping");
-            const int c4 = tid % C4, lr0 = tid / C4, col = cbase + 4 * c4;
-            const bool colv = col + 3 < a.Nc;
-            f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-            if (a.bias && colv) bv = *reinterpret_cast<const f32x4*>(a.bias + col);
-            f32x4 rv[KI];
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const int row = min(r0 + lr0 + k * (NT / C4), a.M - 1);
-                rv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (a.resid && colv) rv[k] = *reinterpret_cast<const f32x4*>(a.resid + (size_t)row * a.ldr + col);
-                else if (a.rx) rv[k] = *reinterpret_cast<const f32x4*>(a.rx + (size_t)row * 4);
-            }
-            float rw[4][4] = {};
-            if (a.rx && colv)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) rw[e][c] = c < a.rxc ? a.rw[(col + e) * a.rxc + c] : 0.f;
-#pragma unroll
-            for (int k = 0; k < KI; ++k) {
-                const int lr = lr0 + k * (NT / C4), row = r0 + lr;
-                if (lr >= RT || row >= a.M || col >= a.Nc) continue;
-                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * C::LDC + 4 * c4);
-                if (colv) {
-                    v += bv;
-                    if (a.rx) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            v[e] += rv[k][0] * rw[e][0] + rv[k][1] * rw[e][1] + rv[k][2] * rw[e][2] + rv[k][3] * rw[e][3];
-                    } else {
-                        v += rv[k];
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : slope * v[e];
-                    *reinterpret_cast<f32x4*>(a.out + (size_t)row * a.ldo + col) = v;
-                } else {
-                    for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
-                        float t = v[e] + (a.bias ? a.bias[col + e] : 0.f);
-                        if (a.resid) t += a.resid[(size_t)row * a.ldr + col + e];
-                        if (a.rx)
-                            for (int c = 0; c < a.rxc; ++c) t = fmaf(a.rx[(size_t)row * 4 + c], a.rw[(col + e) * a.rxc + c], t);
-                        t = t > 0.f ? t : slope * t;
-                        a.out[(size_t)row * a.ldo + col + e] = t;
-                    }
-                }
-            }
-        }
-    }
+    trace_out();
 }
 
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
@@ -339,12 +438,14 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH) || !a.wp || !a.out || a.ldo % 4 ||
         a.nseg < 1 || a.nseg > 2 || a.ksteps != xgemm_ksteps(a) || a.ksteps <= 0)
         return hipErrorInvalidValue;
-    for (int s = 0; s < a.nseg; ++s) {
-        const XSeg& g = a.seg[s];
+    for (int s = 0; s <= a.nseg; ++s) {
+        const XSeg& g = s < a.nseg ? a.seg[s] : a.idn;
+        if (s == a.nseg && !g.src) break;
         if (!g.src || g.cin % 32 || g.ld % 4 || g.ld < g.cin || g.rows_in * g.ld * 4 >= (1LL << 31)) return hipErrorInvalidValue;
     }
-    if (epi == EPI_GRAPH && (a.V != 17 || a.M % 17 || !a.amix || !a.bias)) return hipErrorInvalidValue;
-    if (epi == EPI_BIAS && a.resid && a.ldr % 4) return hipErrorInvalidValue;
+    if (epi == EPI_GRAPH && (a.V != 17 || a.M % 17 || !a.amix || !a.bias || a.idn.src)) return hipErrorInvalidValue;
+    if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
+        return hipErrorInvalidValue;
     if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const int rt = epi == EPI_GRAPH ? 255 : 256;
     const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn), blk(512);

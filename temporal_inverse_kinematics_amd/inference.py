@@ -28,7 +28,10 @@ def run_inference(model, seq_3d_kps: np.ndarray) -> np.ndarray:
     """(F,17,3) keypoints -> (F,66) f32 SMPL-X body pose (inference.py:37-67)."""
     win = model.hparams.win_size
     dev = model.device
-    seq = torch.as_tensor(np.ascontiguousarray(seq_3d_kps, dtype=np.float32), device=dev)
+    if isinstance(seq_3d_kps, torch.Tensor):
+        seq = seq_3d_kps.to(dev, torch.float32).contiguous()
+    else:
+        seq = torch.as_tensor(np.ascontiguousarray(seq_3d_kps, dtype=np.float32), device=dev)
     F = seq.shape[0]
     out = np.empty((F, 66), dtype=np.float32)
     with torch.no_grad():
@@ -55,14 +58,16 @@ def run_test(npz_path: str, smplx_dir: str | None = None, ckpt: str | None = Non
              device="cuda"):
     """inference.run_test:110-145: moveai npz -> COCO -> IK -> (optional) SMPL-X FK."""
     d = np.load(npz_path, allow_pickle=False)
-    seq = kp.moveai3d_to_coco(d["joints_3d"], d["joint_3d_names"].tolist())
+    # the moveai_3d -> COCO conversion on the device (one gather kernel, bit-identical to the host form)
+    seq = kp.moveai3d_to_coco_device(torch.as_tensor(np.ascontiguousarray(d["joints_3d"], dtype=np.float32),
+                                                     device=device), d["joint_3d_names"].tolist())
     if ckpt:
         from .models import IKPoseTrainer
         model = IKPoseTrainer.load_from_checkpoint(ckpt).to(device).eval()
     else:
         model = synthetic_model(win_size, device)
     poses = run_inference(model, seq)
-    result = {"coco": seq, "poses": poses}
+    result = {"coco": seq.cpu().numpy(), "poses": poses}
     if smplx_dir:
         from .smplx_fk import load_smplx_models, run_smpl_inference
         models = load_smplx_models(smplx_dir, device, 9)

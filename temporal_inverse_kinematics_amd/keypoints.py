@@ -5,6 +5,7 @@ from __future__ import annotations
 from typing import List
 
 import numpy as np
+import torch
 
 _COCO_FROM_SMPLX = ["nose", "left_eye", "right_eye", "left_ear", "right_ear", "left_shoulder",
                     "right_shoulder", "left_elbow", "right_elbow", "left_wrist", "right_wrist", "left_hip",
@@ -42,3 +43,19 @@ def moveai3d_to_coco(joints_3d: np.ndarray, joint_names: List[str]) -> np.ndarra
     kps[:, :, 1] = kps[:, :, 2]
     kps[:, :, 2] = -y
     return kps
+
+
+def moveai3d_to_coco_device(joints_3d: torch.Tensor, joint_names: List[str]) -> torch.Tensor:
+    """moveai3d_to_coco on the GPU (tik_moveai_to_coco, one gather kernel):
+    joints_3d (F,J,3) fp32 device -> (F,17,3) device, bit-identical to the host
+    version."""
+    from . import _lib
+    _lib.require_gpu(joints_3d)
+    if joints_3d.dim() != 3 or joints_3d.shape[2] != 3:
+        raise ValueError(f"expected (F,J,3) joints, got {tuple(joints_3d.shape)}")
+    F, J, _ = joints_3d.shape
+    m = (_lib.ctypes.c_int * 17)(*generate_moveai3d_to_coco_mappings(joint_names))
+    out = torch.empty((F, 17, 3), device=joints_3d.device, dtype=torch.float32)
+    _lib.check(_lib.load().tik_moveai_to_coco(joints_3d.data_ptr(), F, J, m, out.data_ptr(),
+                                              _lib.stream_of(joints_3d)), "moveai3d_to_coco_device")
+    return out

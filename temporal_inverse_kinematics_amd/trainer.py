@@ -64,6 +64,8 @@ class GpuTrainer:
             self._names.append((name.value.decode(), tuple(shape[:nd.value]), kind.value))
         self._index = {n: i for i, (n, _, _) in enumerate(self._names)}
         self._loss = torch.zeros(1, device=self.device)
+        # the BatchNorm step counters the model arrived with (checkpoint / earlier training)
+        self._nbt0 = {k: int(v.item()) for k, v in reg.state_dict().items() if k.endswith("num_batches_tracked")}
 
     # ------------------------------------------------------------------ step
     def step(self, keypoints_3d: torch.Tensor, poses: torch.Tensor, dropout_mask: Optional[torch.Tensor] = None,
@@ -91,7 +93,9 @@ class GpuTrainer:
             mptr = dropout_mask.data_ptr()
         _lib.check(lib.tik_trainer_step(self._h.h, x.data_ptr(), N, T, y.data_ptr(), mptr, int(seed) & (2**64 - 1),
                                         self._loss.data_ptr(), _lib.stream_of(x)), "GpuTrainer.step")
-        return self._loss[0]
+        # a fresh tensor per step (the reference returns a new loss each step;
+        # the persistent device buffer is overwritten by the next step)
+        return self._loss[0].clone()
 
     def training_step(self, batch: Dict[str, torch.Tensor], batch_idx: int = 0, dropout_mask=None):
         """pose_trainer.py:146-155 plus Lightning's backward and optimizer step."""
@@ -115,10 +119,9 @@ class GpuTrainer:
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """PoseRegressor state dict after the last step (reference key names)."""
         sd = {n: self.tensor(n) for n, _, _ in self._names}
-        nbt = torch.tensor(self.steps, dtype=torch.long)
-        for k in list(self.regressor.state_dict().keys()):
-            if k.endswith("num_batches_tracked"):
-                sd[k] = nbt.clone()
+        # each BatchNorm counts on from the value it was loaded with (nn.BatchNorm increments its own buffer)
+        for k, v0 in self._nbt0.items():
+            sd[k] = torch.tensor(v0 + self.steps, dtype=torch.long)
         return sd
 
     def grads(self) -> Dict[str, torch.Tensor]:

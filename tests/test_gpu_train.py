@@ -236,3 +236,27 @@ def test_train_step_bitwise_reproducible(lib):
         assert np.array_equal(out[0][1][k], out[1][1][k]), k
     for k in out[0][2]:
         assert np.array_equal(out[0][2][k], out[1][2][k]), k
+
+
+def test_losses_are_fresh_tensors_and_counters_continue(lib):
+    """step() returns a new tensor each step (a kept list of losses
+    does not collapse to the last value), and num_batches_tracked continues from
+    the value the model was loaded with (BatchNorm increments its own buffer)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.trainer import GpuTrainer
+    sd = _weights()
+    m = _model(sd, 9)
+    with torch.no_grad():
+        for k, v in m.regressor.state_dict().items():
+            if k.endswith("num_batches_tracked"):
+                v.fill_(40)
+    tr = GpuTrainer(m, lr=1e-3)
+    rng = np.random.default_rng(3)
+    losses = []
+    for s in range(3):
+        x = torch.from_numpy(syn.synthetic_windows(16, 9, seed=100 + s)).cuda()
+        y = torch.from_numpy(rng.normal(0, 0.5, (16, 1, 66)).astype(np.float32)).cuda()
+        losses.append(tr.step(x, y, seed=s))
+    vals = torch.stack(losses).cpu()
+    assert len(set(vals.tolist())) == 3, vals
+    assert int(tr.state_dict()["backbone.data_bn.num_batches_tracked"]) == 43

@@ -61,6 +61,12 @@ def kernel_symbol(label, precision):
     cgemm.hip tiles are templated on the precision code)."""
     if label in KERNEL_SYMBOLS:
         return KERNEL_SYMBOLS[label]
+    if label == "G0f_raw":
+        return "tik::gcn0_kernel<1, true>"
+    if label[:2] in ("XT", "XG") and label[2:] in ("64", "128"):
+        # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), waves per workgroup (TIK_XNW)>
+        nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
+        return f"tik::xgemm_kernel<{label[2:]}, {0 if label[1] == 'T' else 1}, {nw}>"
     p = PREC_CODE[precision]
     nb_graph = 2 if p == 0 else 1
     cg = {"G272x64": f"272, 64, 1, 4, 1, 17, {p}, {nb_graph}", "T128x128": f"128, 128, 2, 2, 0, 0, {p}, 2",

@@ -103,7 +103,7 @@ int drain_mask() {
 hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, const char* label) {
     static const bool on = getenv("TIK_X_TRACE") != nullptr;
     if (!on) return tik::launch_xgemm(a, bn, epi, st);
-    const int rt = epi == tik::EPI_GRAPH ? 255 : 256;
+    const int rt = tik::xgemm_tile_rows(epi);
     const long long nwg = (long long)((a.M + rt - 1) / rt) * ((a.Nc + bn - 1) / bn);
     unsigned long long* d = nullptr;
     hipError_t e = hipMalloc(&d, nwg * 8 * 8);

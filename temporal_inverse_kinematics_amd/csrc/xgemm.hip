@@ -1,15 +1,19 @@
 // xgemm.hip — bf16x3 implicit GEMM on fp32 activations (see xgemm.h).
 //
-// Tile: 256 rows x BN columns, 8 waves (512 threads), one workgroup per CU.
-// Wave w owns rows 32w..32w+31 (two 16-row fragments) and ALL BN columns, so
-// each A element is read from LDS and split into bf16 planes exactly once per
-// K step, in registers, by the wave that uses it (no split pass, no extra
-// LDS); the weight planes are read by every wave.
+// Tile: BM = 32 NW rows x BN columns. Default NW = 4: a 128-row, 256-thread
+// workgroup of <= 80 KB LDS, TWO per CU, so one workgroup's prologue (first
+// DMA round trip) and epilogue run under the other's main loop (NW = 8, one
+// 256-row workgroup per CU: TIK_XNW=8, 9 % slower end to end). Wave w owns
+// rows 32w..32w+31 (two 16-row fragments) and ALL BN columns, so each A
+// element is read from LDS and split into bf16 planes exactly once per K
+// step, in registers, by the wave that uses it (no split pass, no extra LDS);
+// the weight planes are read by every wave.
 //
-// LDS, per stage: the A image (256 rows x 32 fp32 = 128 B per row) and the B
-// image (3 planes x BN columns x 32 bf16 = 64 B per column). Both are written
-// by LDS-DMA (buffer_load ... lds, 16 B per lane), NST stages deep, one
-// barrier per K step.
+// LDS, per stage: the A image (BM rows x 32 fp32 = 128 B per row) and the B
+// image (3 planes x BN columns x 32 bf16 = 64 B per column), both written by
+// LDS-DMA (buffer_load ... lds, 16 B per lane). A: 2 slots, each wave DMAs
+// its own rows 2 steps ahead (no barrier); B: LB + 1 slots, LB steps ahead,
+// one barrier per K step.
 //  * A row r, logical floats [8g+4h, 8g+4h+4) (g = k group of the MFMA
 //    operand, h = half) at 16-B unit (g + 4h) ^ ((r >> 1) & 7): the two
 //    ds_read_b128 of a fragment read are conflict-free in every lane group.
@@ -19,15 +23,21 @@
 //    conflict-free ds_read_b128 per plane; applied on the host (xgemm_pack).
 // Rows past the batch, and taps outside the window (the temporal zero
 // padding), DMA from an out-of-range offset of the buffer resource: zeros.
+// Inside a step: the next step's A fragments are read first, then per column
+// block the next block's weight reads are issued before this block's 6 FM
+// MFMAs, and fragment i's split for the next step runs between block i's MFMAs.
 //
-// Epilogues stage the fp32 C tile through LDS (half the columns at a time)
-// and store whole 16-B row segments:
-//  * EPI_BIAS: + bias[c] (+ identity residual row, or the layer-0 residual
-//    conv on 4-float rows) -> activation -> out.
-//  * EPI_GRAPH: tiles of 15 whole frames (255 rows); z[f][w] = sum_v A[v][w]
-//    y[f][v] (the einsum of gconv_origin.py:61-63; COCO hop<=2 pattern
-//    unrolled when A_eff fits it) + bias2[w][c], ReLU (st_gcn_aaai18.py:178-179).
+// Epilogues:
+//  * EPI_BIAS (transposed MFMA, so a lane holds 4 channels of a row): + bias
+//    (+ the layer-0 residual conv on 4-float rows) -> activation -> float4
+//    stores straight from registers; the identity residual is added before,
+//    as extra K steps of exact fp32 adds from the DMA'd block-input rows.
+//  * EPI_GRAPH: tiles of whole frames (7 or 15: 119 / 255 rows) staged through
+//    LDS; z[f][w] = sum_v A[v][w] y[f][v] (the einsum of gconv_origin.py:61-63;
+//    COCO hop<=2 pattern unrolled when A_eff fits it) + bias2[w][c], ReLU
+//    (st_gcn_aaai18.py:178-179).
 #include <algorithm>
+#include <cstdlib>
 
 #include "cgemm.h"
 #include "cgemm3_dev.h"
@@ -82,9 +92,13 @@ __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&a
     }
 }
 
-template <int BN, int EPI>
+template <int BN, int EPI, int NW_>
 struct XCfg {
-    static constexpr int NW = 8, NT = 512, BM = 256, FM = 2, FN = BN / 16;
+    // NW waves of 32 rows (two 16-row fragments) each: NW = 8 is one 256-row
+    // workgroup per CU (two waves per SIMD); NW = 4 a 128-row workgroup of
+    // <= 80 KB LDS, two per CU, so one workgroup's prologue and epilogue run
+    // under the other's main loop
+    static constexpr int NW = NW_, NT = 64 * NW, BM = 32 * NW, FM = 2, FN = BN / 16, RW = 32;
     static constexpr bool TR = EPI == EPI_BIAS;   // transposed MFMA: each lane ends with 4 channels of a row
     static constexpr int ABYTES = BM * 128;
     static constexpr int PLANE = BN * 64;
@@ -92,24 +106,29 @@ struct XCfg {
     // A rows are DMA'd and consumed by the same wave (wave w fills and reads rows
     // 32w..32w+31), so the A ring needs no barrier: 2 slots, issued 2 steps ahead
     // (a slot is free once its step's fragments were split, one step early).
-    // B (weights) is shared by all waves: 3 slots, issued 2 steps ahead, one barrier per step.
-    static constexpr int NSA = 2, NSB = 3;
+    // B (weights) is shared by all waves, one barrier per step: issued LB steps
+    // ahead into NSB = LB + 1 slots (LB = 1 for the two-per-CU tile: its wait for
+    // B(k+1) sits after step k's MFMAs, so the DMA has a whole step to land)
+    static constexpr int LB = NW == 8 ? 2 : 1;
+    static constexpr int NSA = 2, NSB = LB + 1;
     static constexpr int RING = NSA * ABYTES + NSB * BBYTES;
     static constexpr int NIA = ABYTES / 1024 / NW;   // A DMA instructions per wave per stage
     static constexpr int NIB_TOT = BBYTES / 1024;
-    static constexpr int RT = EPI == EPI_GRAPH ? 255 : 256;   // valid rows per tile
+    static constexpr int NIBW = (NIB_TOT + NW - 1) / NW;   // B DMA instructions per wave per stage (at most)
+    static constexpr int RT = EPI == EPI_GRAPH ? BM / 17 * 17 : BM;   // valid rows per tile (whole frames for the mix)
     static constexpr int LDCG = BN + 4;
     static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 : 0;
     static constexpr int SMEM = RING > CT ? RING : CT;
-    static_assert(NIA * 1024 * NW == ABYTES, "A DMA split");
-    static_assert(SMEM <= 160 * 1024, "LDS");
+    static constexpr int WG_PER_CU = NW == 8 ? 1 : 2;
+    static_assert(NIA * 1024 * NW == ABYTES && NIA * 8 == RW, "A DMA split");
+    static_assert(SMEM * WG_PER_CU <= 160 * 1024, "LDS");
 };
 
-template <int BN, int EPI>
-__global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
-    using C = XCfg<BN, EPI>;
+template <int BN, int EPI, int NW_>
+__global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs a) {
+    using C = XCfg<BN, EPI, NW_>;
     constexpr int NW = C::NW, NT = C::NT, FM = C::FM, FN = C::FN, NIA = C::NIA, NSA = C::NSA, NSB = C::NSB,
-                  RT = C::RT;
+                  RT = C::RT, RW = C::RW, LB = C::LB;
     constexpr bool TR = C::TR;
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];   // the only LDS object
 
@@ -130,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     const int V = a.V;
 
     // ---- A DMA roles: instruction j of this wave fills rows (wave*NIA + j)*8 + lane/8, unit lane&7
-    // (with NIA = 4 those are rows 32 wave .. 32 wave + 31: exactly the rows this wave computes)
+    // (rows RW wave .. RW wave + RW - 1: exactly the rows this wave computes)
     int a_n[NIA], a_t[NIA], a_w[NIA], a_uo[NIA];
     bool a_ok[NIA];
 #pragma unroll
@@ -149,53 +168,75 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     const int K = a.ksteps;
     // B DMA: a stage's B image is one contiguous packed block; instruction q (of NIB_TOT) copies 1 KB
     const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kmain * C::BBYTES));
-    const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage
+    const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage (NIBW or NIBW - 1)
 
-    // A and B cursors over (segment, tap, 32-channel block); segment a.nseg is the identity residual
-    struct Cur { int seg, tap, blk, k; };
-    auto segof = [&](int sgi) -> XSeg { return sgi == 0 ? a.seg[0] : (sgi == 1 && a.nseg > 1 ? a.seg[1] : a.idn); };
-    auto advance = [&](Cur& c) {
-        const XSeg sg = segof(c.seg);
-        ++c.k;
-        if (++c.blk >= sg.cin / 32) { c.blk = 0; if (++c.tap >= sg.kt) { c.tap = 0; ++c.seg; } }
+    // The A cursor walks (segment, tap, 32-channel block); segment slot 0 =
+    // seg[0], 1 = seg[1] (or the identity when nseg == 1), 2 = the identity.
+    // The per-step advance reads the blocks and taps of each slot from one
+    // packed 64-bit scalar (8 bits each; a select chain over separate values
+    // becomes a scratch lookup table, a dynamically indexed XSeg a kernel-argument
+    // load, every step); the segment's geometry is re-read only when the tap changes.
+    const bool two = a.nseg > 1;
+    const unsigned long long nbkt =
+        (unsigned long long)((a.seg[0].cin >> 5) | (a.seg[0].kt << 8)) |
+        ((unsigned long long)(two ? (a.seg[1].cin >> 5) | (a.seg[1].kt << 8) : (a.idn.cin >> 5) | (a.idn.kt << 8)) << 16) |
+        ((unsigned long long)((a.idn.cin >> 5) | (a.idn.kt << 8)) << 32);
+    int ca_seg = 0, ca_tap = 0, ca_blk = 0, ca_k = 0, cb_k = 0;
+    auto advance_a = [&]() __attribute__((always_inline)) {
+        const unsigned f = (unsigned)(nbkt >> (16 * ca_seg));
+        ++ca_k;
+        if (++ca_blk >= (int)(f & 255u)) {
+            ca_blk = 0;
+            if (++ca_tap >= (int)((f >> 8) & 255u)) { ca_tap = 0; ++ca_seg; }
+        }
     };
-    Cur ca{0, 0, 0, 0}, cb{0, 0, 0, 0};
     unsigned a_off[NIA];
-    i32x4 rA = buf_rsrc(a.seg[0].src, (unsigned)(a.seg[0].rows_in * a.seg[0].ld * 4));
-    int cached_seg = -1, cached_tap = -1;
-    auto prepare = [&]() {
-        if (ca.seg == cached_seg && ca.tap == cached_tap) return;
-        const XSeg sg = segof(ca.seg);
-        if (ca.seg != cached_seg) rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
+    i32x4 rA;
+    bool a_stale = true;   // a_off must be recomputed (a new tap or segment)
+    auto prepare = [&]() __attribute__((always_inline)) {
+        if (!a_stale) return;
+        const XSeg sg = ca_seg == 0 ? a.seg[0] : (ca_seg == 1 && two ? a.seg[1] : a.idn);
+        rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
 #pragma unroll
         for (int j = 0; j < NIA; ++j) {
-            const int t = sg.stride * a_t[j] + ca.tap - sg.pad;
+            const int t = sg.stride * a_t[j] + ca_tap - sg.pad;
             a_off[j] = (a_ok[j] && t >= 0 && t < sg.tin)
                            ? (unsigned)(((a_n[j] * sg.tin + t) * V + a_w[j]) * sg.ld * 4 + a_uo[j])
                            : DMA_OOB;
         }
-        cached_seg = ca.seg; cached_tap = ca.tap;
+        a_stale = false;
     };
-    auto a_slot = [&](int s) { return smem + s * C::ABYTES; };
-    auto b_slot = [&](int s) { return smem + NSA * C::ABYTES + s * C::BBYTES; };
-    auto issue_a = [&]() {   // the A cursor's step, into its ring slot
+    auto a_slot = [&](int s) __attribute__((always_inline)) { return smem + s * C::ABYTES; };
+    auto b_slot = [&](int s) __attribute__((always_inline)) { return smem + NSA * C::ABYTES + s * C::BBYTES; };
+    auto issue_a = [&]() __attribute__((always_inline)) {   // the A cursor's step, into its ring slot
         prepare();
-        unsigned char* A = a_slot(ca.k % NSA);
-        const int soA = __builtin_amdgcn_readfirstlane(ca.blk * 128);
+        unsigned char* A = a_slot(ca_k % NSA);
+        const int soA = __builtin_amdgcn_readfirstlane(ca_blk * 128);
         if (!(a.tune & 1))
 #pragma unroll
             for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
-        advance(ca);
+        const int seg = ca_seg, tap = ca_tap;
+        advance_a();
+        a_stale = ca_seg != seg || ca_tap != tap;
     };
-    auto issue_b = [&]() {   // the B cursor's step (main steps only)
-        unsigned char* B = b_slot(cb.k % NSB);
-        const int soB = __builtin_amdgcn_readfirstlane((ntile * kmain + cb.k) * C::BBYTES);
+    auto issue_b = [&]() __attribute__((always_inline)) {   // weight step cb_k (main steps only)
+        unsigned char* B = b_slot(cb_k % NSB);
+        const int soB = __builtin_amdgcn_readfirstlane((ntile * kmain + cb_k) * C::BBYTES);
         if (!(a.tune & 2))
-            for (int q = wave; q < C::NIB_TOT; q += NW) dma16(rB, B + q * 1024, (unsigned)(q * 1024 + lane * 16), soB);
-        advance(cb);
+#pragma unroll
+            for (int q = 0; q < C::NIBW; ++q)
+                if (q < C::NIBW - 1 || wave + q * NW < C::NIB_TOT)
+                    dma16(rB, B + (wave + q * NW) * 1024, (unsigned)((wave + q * NW) * 1024 + lane * 16), soB);
+        ++cb_k;
     };
-    // VMEM instructions this wave issues for step k (vmcnt accounting)
-    auto n_issued = [&](int k) { return k >= K ? 0 : NIA + (k < kmain ? nbw : 0); };
+    // vmcnt accounting: at step k this wave issues B(k + LB) (nbw instructions,
+    // NIBW or NIBW - 1) then A(k + 2) (NIA); waits count the younger ones
+    auto nA = [&](int k) __attribute__((always_inline)) { return k < K ? NIA : 0; };
+    auto nB = [&](int k) __attribute__((always_inline)) { return k < kmain ? nbw : 0; };
+    auto wait_steady = [&]() __attribute__((always_inline)) {   // NIA + this wave's full B share outstanding
+        if (nbw == C::NIBW) wait_vm<NIA + C::NIBW>();
+        else wait_vm<NIA + C::NIBW - 1>();
+    };
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -205,17 +246,17 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     const int g = lane >> 4;
     const int bsw = (-((lane & 15) >> 2)) & 3;
     const int boff = (lane & 15) * 64 + ((g ^ bsw) << 4);
-    auto mma = [&](const xbf16x8& x, const xbf16x8& w, f32x4& c) {
+    auto mma = [&](const xbf16x8& x, const xbf16x8& w, f32x4& c) __attribute__((always_inline)) {
         // TR: C^T = W . X^T, so lane l holds row (l & 15), channels 4(l >> 4) .. +3
         c = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0)
                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, w, c, 0, 0, 0);
     };
     // this wave's A fragments of a step: fp32 rows -> three bf16 planes
-    auto read_a = [&](int k, f32x4 (&lo)[FM], f32x4 (&hi)[FM]) {
+    auto read_a = [&](int k, f32x4 (&lo)[FM], f32x4 (&hi)[FM]) __attribute__((always_inline)) {
         const unsigned char* A = a_slot(k % NSA);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-            const int r = wave * 32 + i * 16 + (lane & 15);
+            const int r = wave * RW + i * 16 + (lane & 15);
             lo[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + ((g ^ xa_swz(r)) << 4));
             hi[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + (((g + 4) ^ xa_swz(r)) << 4));
         }
@@ -224,15 +265,15 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     f32x4 alo[FM], ahi[FM];
 
     // ---- main steps: the split of step k+1 runs under step k's MFMAs
-    // issue order: B(0) A(0) B(1) A(1) | per step k: B(k+2) A(k+2), so a wait
+    // issue order: B(0) A(0) [B(1)] A(1) | per step k: B(k+LB) A(k+2), so a wait
     // for this wave's A(k) (in issue order) also retires its B(k)
-    if (kmain > 0) issue_b();
+    issue_b();
     issue_a();
-    if (1 < kmain) issue_b();
+    if (LB == 2 && 1 < kmain) issue_b();
     if (1 < K) issue_a();
-    wait_vm_dyn(n_issued(1));   // A(0) (and B(0)) landed
+    wait_vm_dyn(nA(1) + (LB == 2 ? nB(1) : 0));   // A(0) and B(0) landed
     if (tr) t1 = __builtin_amdgcn_s_memtime();
-    if (kmain > 0) {
+    {
         read_a(0, alo, ahi);
 #pragma unroll
         for (int i = 0; i < FM; ++i) xsplit8(alo[i], ahi[i], c0[i], c1[i], c2[i]);
@@ -242,30 +283,40 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     // twice per iteration with the two register sets swapped: no copies)
     xbf16x8 d0[FM], d1[FM], d2[FM];
     auto main_step = [&](int k, xbf16x8 (&u0)[FM], xbf16x8 (&u1)[FM], xbf16x8 (&u2)[FM], xbf16x8 (&v0)[FM],
-                         xbf16x8 (&v1)[FM], xbf16x8 (&v2)[FM]) {
+                         xbf16x8 (&v1)[FM], xbf16x8 (&v2)[FM]) __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const unsigned long long tb0 = tr ? __builtin_amdgcn_s_memtime() : 0;
         __builtin_amdgcn_s_barrier();   // every wave's B(k) landed; every wave done reading B(k-1)
         if (tr) t_bar += __builtin_amdgcn_s_memtime() - tb0;
-        if (k + 2 < kmain) issue_b();
+        if (k + LB < kmain) issue_b();
         if (k + 2 < K) issue_a();
-        // this wave's A(k+1) landed (B(k+2), A(k+2) may still fly); past the last
+        // this wave's A(k+1) landed (B(k+LB), A(k+2) may still fly); past the last
         // step the read + split below run on a stale slot and are discarded
         {
             const unsigned long long tv0 = tr ? __builtin_amdgcn_s_memtime() : 0;
-            wait_vm_dyn(n_issued(k + 2));
+            if (k + 2 < kmain) wait_steady();
+            else wait_vm_dyn(nB(k + LB) + nA(k + 2));
             if (tr) t_vm += __builtin_amdgcn_s_memtime() - tv0;
         }
         const unsigned char* B = b_slot(k % NSB) + boff;
-        // one scheduling region: step k's MFMAs with step k+1's A reads and split
-        // and step k's B reads interleaved between them (sched_group_barrier below)
+        // Software pipeline inside the step: the A reads of step k+1 and the
+        // first weight block's reads, then per column block j the next block's
+        // reads are issued BEFORE the 6 FM MFMAs of j (so no read is waited on
+        // right after its issue), and fragment j's split of step k+1 runs
+        // between block j's MFMAs. sched_barriers keep the blocks in this order.
+        xbf16x8 bb[2][3];
         __builtin_amdgcn_sched_barrier(0);
         read_a(k + 1, alo, ahi);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            xbf16x8 b[3];
+        for (int p = 0; p < 3; ++p) bb[0][p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE + j * 16 * 64);
+        for (int j = 0; j < FN; ++j) {
+            if (j + 1 < FN)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bb[(j + 1) & 1][p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE + (j + 1) * 16 * 64);
+            const xbf16x8(&b)[3] = bb[j & 1];
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 mma(u2[i], b[0], acc[i][j]);
@@ -275,20 +326,24 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
                 mma(u0[i], b[1], acc[i][j]);
                 mma(u0[i], b[0], acc[i][j]);
             }
-            if (j == 0)
+            if (j < FM && !(a.tune & 8)) xsplit8(alo[j], ahi[j], v0[j], v1[j], v2[j]);
+            // past the last block the remaining fragments' splits
+            if (j == FN - 1)
 #pragma unroll
-                for (int i = 0; i < FM; ++i) xsplit8(alo[i], ahi[i], v0[i], v1[i], v2[i]);
-        }
-        // pattern: the A reads and the first B block's reads, then per MFMA up to two
-        // VALU and, every third MFMA, one LDS read
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * FM + 3, 0);
+                for (int i = FN; i < FM; ++i) xsplit8(alo[i], ahi[i], v0[i], v1[i], v2[i]);
+            if (j + 1 < FN) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
-        for (int q = 0; q < 6 * FM * FN; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if (q % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            for (int q = 0; q < 6 * FM; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (LB == 1) {   // B(k+1) landed before the next step's barrier (only A(k+2) younger)
+            const unsigned long long tv0 = tr ? __builtin_amdgcn_s_memtime() : 0;
+            wait_vm_dyn(nA(k + 2));
+            if (tr) t_vm += __builtin_amdgcn_s_memtime() - tv0;
+        }
     };
     for (int k = 0; k < kmain; k += 2) {
         main_step(k, c0, c1, c2, d0, d1, d2);
@@ -305,7 +360,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
             f32x4 xv[FM][2];
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const int r = wave * 32 + i * 16 + (lane & 15);
+                const int r = wave * RW + i * 16 + (lane & 15);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     // channels 32 blk + 16h + 4g .. +3 = logical floats [8 g' + 4 h', +4)
@@ -327,7 +382,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tr) t3 = __builtin_amdgcn_s_memtime();
-    auto trace_out = [&]() {
+    auto trace_out = [&]() __attribute__((always_inline)) {
         if (tr && tid == 0) {
             unsigned long long* o = a.trace + 8 * (size_t)(blockIdx.y * gridDim.x + blockIdx.x);
             o[0] = t1 - t0; o[1] = t2 - t1; o[2] = t3 - t2; o[3] = __builtin_amdgcn_s_memtime() - t3;
@@ -343,7 +398,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
         bool rok[FM];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-            const int lr = wave * 32 + i * 16 + (lane & 15);
+            const int lr = wave * RW + i * 16 + (lane & 15);
             rok[i] = lr < RT && r0 + lr < a.M;
             rows[i] = rok[i] ? r0 + lr : 0;
         }
@@ -392,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     } else {
         // ---- EPI_GRAPH: the C tile through LDS, then the graph mix per frame
         float* Cs = reinterpret_cast<float*>(smem);
-        const int crow = wave * 32 + 4 * g;
+        const int crow = wave * RW + 4 * g;
         const int ccol = lane & 15;
         __syncthreads();   // every wave done with the K loop's LDS
 #pragma unroll
@@ -407,13 +462,13 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) amv[k] = 64 * k + lane < 17 * 17 ? a.amix[64 * k + lane] : 0.f;
         __syncthreads();
-        // waves 0-3 produce joints 0-8, waves 4-7 joints 9-16 (wave-uniform split,
+        // the first half of the waves produce joints 0-8, the second joints 9-16 (wave-uniform split,
         // so each half's joint loop is compile-time); item = (frame, 4 columns)
         constexpr int C4 = BN / 4;
         const int nframes = a.M / 17, f0 = r0 / 17;
         const bool second = wave >= NW / 2;
 #pragma unroll 1
-        for (int it = tid & (NT / 2 - 1); it < 15 * C4; it += NT / 2) {
+        for (int it = tid & (NT / 2 - 1); it < RT / 17 * C4; it += NT / 2) {
             const int f = it / C4, c4 = it - f * C4;
             const int col = n0 + 4 * c4;
             if (f0 + f >= nframes || col >= a.Nc) continue;
@@ -433,10 +488,20 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(XArgs a) {
     trace_out();
 }
 
+int xgemm_waves() {   // TIK_XNW=4|8 (default 4: two workgroups per CU, 278k vs 254k IK frames/s): waves per workgroup (see XCfg)
+    static const int nw = [] { const char* e = getenv("TIK_XNW"); return e && atoi(e) == 8 ? 8 : 4; }();
+    return nw;
+}
+
+int xgemm_tile_rows(int epi) {
+    const int bm = 32 * xgemm_waves();
+    return epi == EPI_GRAPH ? bm / 17 * 17 : bm;
+}
+
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH) || !a.wp || !a.out || a.ldo % 4 ||
-        a.nseg < 1 || a.nseg > 2 || a.ksteps != xgemm_ksteps(a) || a.ksteps <= 0)
+        a.nseg < 1 || a.nseg > 2 || a.ksteps != xgemm_ksteps(a) || xgemm_kmain(a) <= 0)
         return hipErrorInvalidValue;
     for (int s = 0; s <= a.nseg; ++s) {
         const XSeg& g = s < a.nseg ? a.seg[s] : a.idn;
@@ -447,16 +512,18 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
     if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
-    const int rt = epi == EPI_GRAPH ? 255 : 256;
-    const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn), blk(512);
+    const int nw = xgemm_waves(), rt = xgemm_tile_rows(epi);
+    const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn), blk(64 * nw);
     (void)hipGetLastError();
-    if (bn == 128) {
-        if (epi == EPI_BIAS) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((xgemm_kernel<128, EPI_GRAPH>), grid, blk, 0, st, a);
+#define XL(BN_, EPI_, NW__) hipLaunchKernelGGL((xgemm_kernel<BN_, EPI_, NW__>), grid, blk, 0, st, a)
+    if (nw == 4) {
+        if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 4); else XL(128, EPI_GRAPH, 4); }
+        else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 4); else XL(64, EPI_GRAPH, 4); }
     } else {
-        if (epi == EPI_BIAS) hipLaunchKernelGGL((xgemm_kernel<64, EPI_BIAS>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((xgemm_kernel<64, EPI_GRAPH>), grid, blk, 0, st, a);
+        if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 8); else XL(128, EPI_GRAPH, 8); }
+        else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 8); else XL(64, EPI_GRAPH, 8); }
     }
+#undef XL
     return hipGetLastError();
 }
 

@@ -73,15 +73,23 @@ int tik_model_out_frames(tik_model_t m, int T);
 int tik_model_reserve(tik_model_t m, int N, int T);
 /* keypoints x: (N,T,V=17,C=3) fp32 device; poses: (N,T',66) fp32 device. */
 int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, void* stream);
-/* Backbone only (StgGcn18.forward, st_gcn_aaai18.py:113-133): feat (N,T',V*Cout). */
+/* Backbone only (StgGcn18.forward, st_gcn_aaai18.py:113-133): feat (N,T',V*Cout).
+ * A handle created from a backbone-only state dict (StgGcn18's own keys, no
+ * head) serves this call only; tik_ik_forward and tik_stream_create refuse it. */
 int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream);
 
-/* GEMM arithmetic: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
- * 1 = 3-term f16 split (v_mfma_f32_16x16x32_f16 on x = hi + lo, fp32
- * accumulate; ~2^-22 relative per product). Default 1, or 0 when the
- * environment sets TIK_PRECISION=fp32 at handle creation. */
+/* GEMM arithmetic (all accumulate in fp32):
+ * 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
+ * 1 = 3-term f16 split (v_mfma_f32_16x16x32_f16 on x = hi + lo; f16's
+ *     exponent range: |x| > 65504 overflows, small values lose bits);
+ * 2 = 6-product bf16 split (v_mfma_f32_16x16x32_bf16 on x = p0 + p1 + p2,
+ *     products p_i q_j with i + j <= 2: fp32's exponent range, ~2^-24
+ *     relative per product) — the DEFAULT.
+ * The environment variable TIK_PRECISION=fp32|f16x3|bf16x3 picks the
+ * arithmetic at handle creation. */
 #define TIK_PREC_F32 0
 #define TIK_PREC_F16X3 1
+#define TIK_PREC_BF16X3 2
 int tik_model_set_precision(tik_model_t m, int prec);
 int tik_model_get_precision(tik_model_t m);
 

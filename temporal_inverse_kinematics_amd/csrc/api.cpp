@@ -103,7 +103,7 @@ int drain_mask() {
 hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, const char* label) {
     static const bool on = getenv("TIK_X_TRACE") != nullptr;
     if (!on) return tik::launch_xgemm(a, bn, epi, st);
-    const int rt = tik::xgemm_tile_rows(epi);
+    const int rt = tik::xgemm_tile_rows(epi, a.nw);
     const long long nwg = (long long)((a.M + rt - 1) / rt) * ((a.Nc + bn - 1) / bn);
     unsigned long long* d = nullptr;
     hipError_t e = hipMalloc(&d, nwg * 8 * 8);
@@ -227,6 +227,7 @@ struct Layer {
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
+    int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -392,7 +393,7 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune();
+            g.tune = xtune(); g.nw = xnw;
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
@@ -418,7 +419,7 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune();
+        t.tune = xtune(); t.nw = xnw;
         const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
@@ -887,6 +888,8 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
     if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
     if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
+    if (const char* e = getenv("TIK_XNW"))
+        for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);

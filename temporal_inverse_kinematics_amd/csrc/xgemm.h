@@ -50,6 +50,7 @@ struct XArgs {
     float* out;                 // fp32 [M][ldo]
     int ldo;
     int act;
+    int nw;     // waves per workgroup: 4 (or 0: two 128-row workgroups per CU) or 8 (one 256-row workgroup)
     int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA, 8 skip the split
     unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null
 };
@@ -65,8 +66,7 @@ __host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain
 // epi: EPI_BIAS (cgemm.h: bias + residual + activation) or EPI_GRAPH (graph
 // mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
-int xgemm_waves();              // waves per workgroup of the launches (4, or 8 with TIK_XNW=8)
-int xgemm_tile_rows(int epi);   // output rows per workgroup (whole frames for EPI_GRAPH)
+int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
 
 // Host packing of the weights of up to two segments (segment s: fp32
 // W_s[n][tap * cin_s + c], row stride ldw_s) into the tile layout above,

@@ -71,13 +71,15 @@ __device__ __forceinline__ float xam(const float (&amv)[5], int i) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[i / 64]), i % 64));
 }
 
-template <int W0, int W1, bool SPARSE>
+// bias2 is the tile's [17][BN] slice staged in LDS (a global load between the
+// stores would wait for every store before it: vmcnt counts both)
+template <int W0, int W1, bool SPARSE, int BN>
 __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&amv)[5],
-                                           const float* __restrict__ bias2, int Nc, int col, float* __restrict__ o,
+                                           const float* __restrict__ bias2s, int lcol, float* __restrict__ o,
                                            int ldo) {
 #pragma unroll
     for (int w = W0; w < W1; ++w) {
-        f32x4 z = *reinterpret_cast<const f32x4*>(bias2 + w * Nc + col);
+        f32x4 z = *reinterpret_cast<const f32x4*>(bias2s + w * BN + lcol);
         if constexpr (SPARSE) {
 #pragma unroll
             for (int v = 0; v < 17; ++v)
@@ -117,7 +119,7 @@ struct XCfg {
     static constexpr int NIBW = (NIB_TOT + NW - 1) / NW;   // B DMA instructions per wave per stage (at most)
     static constexpr int RT = EPI == EPI_GRAPH ? BM / 17 * 17 : BM;   // valid rows per tile (whole frames for the mix)
     static constexpr int LDCG = BN + 4;
-    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 : 0;
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : 0;   // C tile + bias2 slice
     static constexpr int SMEM = RING > CT ? RING : CT;
     static constexpr int WG_PER_CU = NW == 8 ? 1 : 2;
     static_assert(NIA * 1024 * NW == ABYTES && NIA * 8 == RW, "A DMA split");
@@ -128,7 +130,7 @@ template <int BN, int EPI, int NW_>
 __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs a) {
     using C = XCfg<BN, EPI, NW_>;
     constexpr int NW = C::NW, NT = C::NT, FM = C::FM, FN = C::FN, NIA = C::NIA, NSA = C::NSA, NSB = C::NSB,
-                  RT = C::RT, RW = C::RW, LB = C::LB;
+                  RT = C::RT, RW = C::RW, LB = C::LB, BM = C::BM;
     constexpr bool TR = C::TR;
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];   // the only LDS object
 
@@ -147,6 +149,16 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     }
     const int n0 = ntile * BN;
     const int V = a.V;
+    // EPI_GRAPH: this tile's bias2[17][n0 .. n0 + BN) slice, loaded now so its
+    // latency hides under the K loop (staged in LDS by the epilogue)
+    constexpr int NB2 = EPI == EPI_GRAPH ? (17 * BN / 4 + NT - 1) / NT : 0;
+    f32x4 b2r[NB2 > 0 ? NB2 : 1];
+#pragma unroll
+    for (int u = 0; u < NB2; ++u) {
+        const int q = tid + u * NT, w = q / (BN / 4), c = 4 * (q - w * (BN / 4));
+        b2r[u] = q < 17 * BN / 4 && n0 + c + 3 < a.Nc ? *reinterpret_cast<const f32x4*>(a.bias + w * a.Nc + n0 + c)
+                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     // ---- A DMA roles: instruction j of this wave fills rows (wave*NIA + j)*8 + lane/8, unit lane&7
     // (rows RW wave .. RW wave + RW - 1: exactly the rows this wave computes)
@@ -408,18 +420,37 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (a.rx) xr[i] = *reinterpret_cast<const f32x4*>(a.rx + (size_t)rows[i] * 4);
         }
+        // every global operand is loaded before the first store: a load issued
+        // after a store waits for that store too (vmcnt counts both, in order)
+        f32x4 bvs[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + 16 * j + 4 * g;
+            bvs[j] = a.bias && col + 3 < a.Nc ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // layer 0's residual conv weights (BN 64 tiles only, launch_xgemm checks)
+        constexpr int FNR = BN == 64 ? FN : 1;
+        float rws[FNR][4][4];
+#pragma unroll
+        for (int j = 0; j < FNR; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int col = n0 + 16 * j + 4 * g + e;
+                    rws[j][e][c] = BN == 64 && a.rx && c < a.rxc && col < a.Nc ? a.rw[col * a.rxc + c] : 0.f;
+                }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
             const int col = n0 + 16 * j + 4 * g;
             if (col >= a.Nc) continue;
             if (col + 3 < a.Nc) {
-                const f32x4 bv = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-                float rw[4][4] = {};
-                if (a.rx)
+                const f32x4 bv = bvs[j];
+                float rw[4][4];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) rw[e][c] = c < a.rxc ? a.rw[(col + e) * a.rxc + c] : 0.f;
+                    for (int c = 0; c < 4; ++c) rw[e][c] = rws[j % FNR][e][c];
 #pragma unroll
                 for (int i = 0; i < FM; ++i) {
                     f32x4 v = acc[i][j] + bv;
@@ -456,6 +487,12 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             for (int j = 0; j < FN; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) Cs[(crow + i * 16 + e) * C::LDCG + j * 16 + ccol] = acc[i][j][e];
+        float* b2s = Cs + BM * C::LDCG;   // bias2[w][n0 .. n0 + BN) (loaded at kernel start)
+#pragma unroll
+        for (int u = 0; u < NB2; ++u) {
+            const int q = tid + u * NT;
+            if (q < 17 * BN / 4) *reinterpret_cast<f32x4*>(b2s + 4 * q) = b2r[u];
+        }
         // A_eff in 5 VGPRs across the wave, read back with v_readlane (global loads
         // would be re-issued after every store, which may alias them)
         float amv[5];
@@ -477,24 +514,19 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             for (int v = 0; v < 17; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * 17 + v) * C::LDCG + 4 * c4);
             float* o = a.out + (size_t)(f0 + f) * 17 * a.ldo + col;
             if (a.mix_sparse) {
-                if (second) xmix_store<9, 17, true>(y, amv, a.bias, a.Nc, col, o, a.ldo);
-                else xmix_store<0, 9, true>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+                if (second) xmix_store<9, 17, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
+                else xmix_store<0, 9, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
             } else {
-                if (second) xmix_store<9, 17, false>(y, amv, a.bias, a.Nc, col, o, a.ldo);
-                else xmix_store<0, 9, false>(y, amv, a.bias, a.Nc, col, o, a.ldo);
+                if (second) xmix_store<9, 17, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
+                else xmix_store<0, 9, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
             }
         }
     }
     trace_out();
 }
 
-int xgemm_waves() {   // TIK_XNW=4|8 (default 4: two workgroups per CU, 278k vs 254k IK frames/s): waves per workgroup (see XCfg)
-    static const int nw = [] { const char* e = getenv("TIK_XNW"); return e && atoi(e) == 8 ? 8 : 4; }();
-    return nw;
-}
-
-int xgemm_tile_rows(int epi) {
-    const int bm = 32 * xgemm_waves();
+int xgemm_tile_rows(int epi, int nw) {
+    const int bm = 32 * (nw == 8 ? 8 : 4);
     return epi == EPI_GRAPH ? bm / 17 * 17 : bm;
 }
 
@@ -509,10 +541,12 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
         if (!g.src || g.cin % 32 || g.ld % 4 || g.ld < g.cin || g.rows_in * g.ld * 4 >= (1LL << 31)) return hipErrorInvalidValue;
     }
     if (epi == EPI_GRAPH && (a.V != 17 || a.M % 17 || !a.amix || !a.bias || a.idn.src)) return hipErrorInvalidValue;
+    if (a.rx && (bn != 64 || epi != EPI_BIAS || a.rxc < 0 || a.rxc > 4)) return hipErrorInvalidValue;
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
     if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
-    const int nw = xgemm_waves(), rt = xgemm_tile_rows(epi);
+    const int nw = a.nw == 8 ? 8 : 4, rt = xgemm_tile_rows(epi, nw);
+    if (a.nw != 0 && a.nw != 4 && a.nw != 8) return hipErrorInvalidValue;
     const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn), blk(64 * nw);
     (void)hipGetLastError();
 #define XL(BN_, EPI_, NW__) hipLaunchKernelGGL((xgemm_kernel<BN_, EPI_, NW__>), grid, blk, 0, st, a)

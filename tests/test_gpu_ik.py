@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
+@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xnw8", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
                                                  "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
                                                  "f16x3-dmahead"])
 def model(request):
@@ -41,7 +41,9 @@ def model(request):
                # bf16x3 on the register-staged cgemm.hip tiles instead of xgemm.hip
                "cgemm": {"TIK_XGEMM": "0"},
                # xgemm in sub-batches of at most 3 windows (the 2 GiB-per-tensor split)
-               "xchunk": {"TIK_DMA_CHUNK": "3"}}.get(path, {"TIK_GEMM_PATH": path})
+               "xchunk": {"TIK_DMA_CHUNK": "3"},
+               # xgemm with one 256-row, 8-wave workgroup per CU (default: two 128-row ones)
+               "xnw8": {"TIK_XNW": "8"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created

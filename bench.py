@@ -63,10 +63,12 @@ def kernel_symbol(label, precision):
         return KERNEL_SYMBOLS[label]
     if label == "G0f_raw":
         return "tik::gcn0_kernel<1, true>"
-    if label[:2] in ("XT", "XG") and label[2:] in ("64", "128"):
+    if label[:2] in ("XT", "XG", "XH") and label[2:] in ("64", "128"):
         # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), waves per workgroup (TIK_XNW)>
         nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
-        return f"tik::xgemm_kernel<{label[2:]}, {0 if label[1] == 'T' else 1}, {nw}>"
+        return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
+    if label == "XR":
+        return "tik::xgemm_splitk_reduce_kernel"
     p = PREC_CODE[precision]
     nb_graph = 2 if p == 0 else 1
     cg = {"G272x64": f"272, 64, 1, 4, 1, 17, {p}, {nb_graph}", "T128x128": f"128, 128, 2, 2, 0, 0, {p}, 2",
@@ -230,7 +232,7 @@ def main():
         gathers.drain()
         lib = _lib.load()
         h = reg.tik_handle()
-        per_fwd = 2 * len(reg.backbone.st_gcn_networks) + 3
+        per_fwd = 2 * len(reg.backbone.st_gcn_networks) + 4
 
         def timed(k):
             """k steps between barrier + synchronize on both sides; max over ranks"""

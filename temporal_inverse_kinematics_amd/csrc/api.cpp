@@ -228,6 +228,7 @@ struct Layer {
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
+    int xepi = 1;           // xgemm EPI_BIAS epilogue through LDS, whole-line stores (TIK_XEPI=0: from registers)
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -379,7 +380,7 @@ struct Layer {
     // ([rows][4]) for the residual conv in the temporal conv's epilogue.
     int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st,
                   const float* xraw = nullptr, const float* bn_sc = nullptr, const float* bn_sh = nullptr,
-                  float* xb4 = nullptr) const {
+                  float* xb4 = nullptr, hipEvent_t ev_g = nullptr) const {
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         const double px_in = (double)rin, px_out = (double)rout;
@@ -400,6 +401,7 @@ struct Layer {
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
+        if (ev_g) HIP_TRY(hipEventRecord(ev_g, st));   // split-batch lag point (backbone_x)
         tik::XArgs t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
         t.seg[0] = tik::XSeg{z, cout, cout, TK, stride, 1, tin, rin};
@@ -419,7 +421,7 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune(); t.nw = xnw;
+        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi;
         const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
@@ -716,6 +718,8 @@ struct tik_model {
     SplitW sw0, sw3;
     SplitW3 s30, s33;
     SBW sb0, sb3;
+    DevHBuf xh0;                   // bf16x3 tiles of pose_regressor.0 for xgemm.hip (feat % 32 == 0)
+    int xhead_wgs = 512;           // xgemm head: split K until this many workgroups (TIK_XHEAD_WGS; 0: the cgemm head)
     int prec = 1;
     // ws[0]: the handle's workspace (z, z2: ping-pong for the fused T+G launches);
     // ws[1] + a private stream: large f16x3 batches run as two halves on two
@@ -727,6 +731,7 @@ struct tik_model {
     hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT - 1] = {};
     bool split = true;                 // TIK_SPLIT=0: one stream
     int nsplit = 2;                    // parts of a split batch (TIK_SPLIT_N, 2..4)
+    int split_lag = 0;                 // xgemm path: parts 1.. start after part 0's launch number split_lag (TIK_SPLIT_LAG)
     std::atomic<int> refs{1};          // the handle + every live online-IK stream
     ~tik_model() {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -890,7 +895,10 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
     if (const char* e = getenv("TIK_XNW"))
         for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
+    if (const char* e = getenv("TIK_XEPI"))
+        for (auto& L : md->layers) L.xepi = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
+    if (const char* e = getenv("TIK_SPLIT_LAG")) md->split_lag = std::max(0, atoi(e));
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
     if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
     if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
@@ -906,6 +914,11 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         (rc = md->s33.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
         delete md;
         return rc;
+    }
+    if (const char* e = getenv("TIK_XHEAD_WGS")) md->xhead_wgs = atoi(e);
+    if (md->feat % 32 == 0) {
+        const tik::XPackSeg h{W0->v.data(), md->feat, 1, md->feat};
+        if ((rc = md->xh0.upload(tik::xgemm_pack(&h, 1, md->hidden, 128)))) { delete md; return rc; }
     }
     *out = md;
     return TIK_OK;
@@ -936,9 +949,10 @@ int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
     }
     int rc;
     // split-K partials: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
+    // (cgemm), or up to 8 K slices of the xgemm head's hidden rows
     if ((rc = w.xb.reserve((size_t)N * T * V * 32)) || (rc = w.z.reserve(zmax)) || (rc = w.z2.reserve(zmax)) ||
         (rc = w.a0.reserve(amax)) || (rc = w.a1.reserve(amax)) || (rc = w.hid.reserve((size_t)N * t * m->hidden)) ||
-        (rc = w.part.reserve((size_t)384 * 128 * 128)))
+        (rc = w.part.reserve(std::max((size_t)384 * 128 * 128, (size_t)8 * N * t * m->hidden))))
         return rc;
     return TIK_OK;
 }
@@ -1065,17 +1079,22 @@ static int x_chunk(const tik_model* m, int T) {
 
 // Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
 // from the raw keypoints (data_bn folded into its gcn kernel).
+// ev (split batches, part 0 only): recorded after launch number `lag` of the
+// backbone (G of layer l = launch 2l + 1, its T = 2l + 2), so the other parts
+// start that many launches behind and their G and T launches interleave.
 static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st,
-                      const WsPtrs& w) {
+                      const WsPtrs& w, int lag = 0, hipEvent_t ev = nullptr) {
     const float* cur = nullptr;
     int ld = 0, t = T, rc;
     float* bufs[2] = {w.a0, w.a1};
     int which = 0;
     for (const Layer& L : m->layers) {
         float* o = bufs[which];
-        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb);
-        else rc = L.forward_x(cur, ld, N, t, w.z, o, st);
+        hipEvent_t eg = ev && lag == 2 * L.index + 1 ? ev : nullptr;
+        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb, eg);
+        else rc = L.forward_x(cur, ld, N, t, w.z, o, st, nullptr, nullptr, nullptr, nullptr, eg);
         if (rc) return rc;
+        if (ev && lag == 2 * L.index + 2) HIP_TRY(hipEventRecord(ev, st));
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);
@@ -1193,6 +1212,8 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
     return TIK_OK;
 }
 
+static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st);
+
 // Head on fp32 features with split-K (few rows: the K = 4352 loop spread over
 // workgroups instead of run serially by the handful of row tiles).
 static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, float* part, hipStream_t st) {
@@ -1207,6 +1228,11 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
                      4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
         HIP_TRY(tik::launch_cgemm(h, tik::CFG_H64x64, st, m->prec));
     }
+    return head3_splitk(m, hid, rows, poses, part, st);
+}
+
+// the head's second layer (hidden -> pose_dim, pose_trainer.py:92) with split-K
+static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st) {
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
     p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->s33, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
@@ -1219,6 +1245,40 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
         HIP_TRY(tik::launch_cgemm(p, tik::CFG_H64x64, st, m->prec));
     }
     return TIK_OK;
+}
+
+// Head of the bf16x3 path: pose_regressor.0 (feat -> hidden, LeakyReLU,
+// pose_trainer.py:89-91) on xgemm.hip, its K = feat loop split over enough
+// workgroups to fill the chip (the frames are few: 4096 rows at B = 1024) and
+// the slices summed in a fixed order by the reduce kernel (+ bias, LeakyReLU);
+// then pose_regressor.3 with split-K as head_splitk.
+static int head_x(tik_model_t m, const float* f, int rows, float* poses, const WsPtrs& w, hipStream_t st) {
+    if (!m->xh0.p || m->xhead_wgs <= 0) return head_splitk(m, f, rows, poses, w.hid, w.part, st);
+    tik::XArgs h{};
+    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
+    h.seg[0] = tik::XSeg{f, m->feat, m->feat, 1, 1, 0, rows, rows};
+    h.nseg = 1; h.wp = m->xh0.p; h.ksteps = tik::xgemm_ksteps(h);
+    h.nw = m->layers.front().xnw; h.epi_lds = m->layers.front().xepi;
+    const int tiles = ((rows + tik::xgemm_tile_rows(tik::EPI_BIAS, h.nw) - 1) / tik::xgemm_tile_rows(tik::EPI_BIAS, h.nw)) *
+                      ((m->hidden + 127) / 128);
+    h.ksplit = std::min(8, tik::xgemm_splitk_for(tiles, h.ksteps, m->xhead_wgs));
+    if (h.ksplit > 1) {
+        h.out = w.part; h.act = tik::ACT_NONE;
+    } else {
+        h.out = w.hid; h.bias = m->b0.p; h.act = tik::ACT_LEAKY;
+    }
+    h.ldo = m->hidden;
+    {
+        ProfScope pr("XH128.head0", 2.0 * rows * m->feat * m->hidden,
+                     4.0 * ((double)rows * (m->feat + (double)h.ksplit * m->hidden) + (double)m->feat * m->hidden), st);
+        HIP_TRY(tik::launch_xgemm(h, 128, tik::EPI_BIAS, st));
+    }
+    if (h.ksplit > 1) {
+        ProfScope pr("XR.head0", (double)rows * m->hidden * h.ksplit, 4.0 * (double)rows * m->hidden * (h.ksplit + 1), st);
+        HIP_TRY(tik::launch_xgemm_splitk_reduce(w.part, h.ksplit, rows, m->hidden, m->b0.p, tik::ACT_LEAKY, w.hid,
+                                                m->hidden, st));
+    }
+    return head3_splitk(m, w.hid, rows, poses, w.part, st);
 }
 
 }  // extern "C"
@@ -1276,12 +1336,45 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
     if (use_x(m)) {
         const int chunk = std::min(N, x_chunk(m, T));
         if ((rc = model_reserve_ws(m, ws, chunk, T))) return rc;
-        const WsPtrs w = ptrs_of(ws);
         const int To = tik_model_out_frames(m, T);
+        // large batches: np parts on np streams (the caller's + handle-owned
+        // ones, fork/join by events), so one part's HBM-bound graph launches
+        // run beside another part's MFMA-bound temporal convs (not while
+        // profiling: per-launch events would time overlapping kernels)
+        const bool split = allow_split && m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
+        const int np = split ? std::min(m->nsplit, std::min(N, chunk)) : 1;
+        if (split && (rc = reserve_parts(m, np, (std::min(N, chunk) + np - 1) / np, T))) return rc;
+        const int lag = m->split_lag;
+        auto part = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w, hipEvent_t ev) -> int {
+            float* fs;
+            int r;
+            if ((r = backbone_x(m, xs, n, T, &fs, &to, s, w, lag, ev))) return r;
+            return head_x(m, fs, n * to, ps, w, s);
+        };
         for (int n0 = 0; n0 < N; n0 += chunk) {
             const int n = std::min(chunk, N - n0);
-            if ((rc = backbone_x(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &to, st, w))) return rc;
-            if ((rc = head_splitk(m, f, n * to, poses + (size_t)n0 * To * m->pose_dim, w.hid, w.part, st))) return rc;
+            const float* xs = x + (size_t)n0 * T * m->V * m->C0;
+            float* ps = poses + (size_t)n0 * To * m->pose_dim;
+            if (split && n >= np && (long long)n * T >= 32768) {
+                // the other parts start after part 0's launch number `lag`
+                // (0: together, at the fork), so their G and T launches interleave
+                if (lag <= 0) HIP_TRY(hipEventRecord(m->ev_fork, st));
+                for (int k = 0; k < np; ++k) {
+                    const int a0 = (int)((long long)n * k / np), a1 = (int)((long long)n * (k + 1) / np);
+                    if (k == 1)
+                        for (int j = 1; j < np; ++j) HIP_TRY(hipStreamWaitEvent(m->aux[j - 1], m->ev_fork, 0));
+                    if ((rc = part(xs + (size_t)a0 * T * m->V * m->C0, a1 - a0, ps + (size_t)a0 * To * m->pose_dim,
+                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]),
+                                   k == 0 && lag > 0 ? m->ev_fork : nullptr)))
+                        return rc;
+                }
+                for (int k = 1; k < np; ++k) {
+                    HIP_TRY(hipEventRecord(m->ev_join[k - 1], m->aux[k - 1]));
+                    HIP_TRY(hipStreamWaitEvent(st, m->ev_join[k - 1], 0));
+                }
+            } else if ((rc = part(xs, n, ps, st, ptrs_of(ws), nullptr))) {
+                return rc;
+            }
         }
         return TIK_OK;
     }

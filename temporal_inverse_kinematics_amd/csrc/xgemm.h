@@ -50,6 +50,11 @@ struct XArgs {
     float* out;                 // fp32 [M][ldo]
     int ldo;
     int act;
+    // split K (EPI_BIAS, one kt-1 segment, no residual, bias or activation):
+    // blockIdx.z = k slice; slice z writes its raw partial sums to
+    // out + z * M * ldo, and xgemm_splitk_reduce finishes (0 or 1: no split)
+    int ksplit;
+    int epi_lds;  // EPI_BIAS: stage the C tile through LDS for whole-line row-major stores (else float4 stores from registers)
     int nw;     // waves per workgroup: 4 (or 0: two 128-row workgroups per CU) or 8 (one 256-row workgroup)
     int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA, 8 skip the split
     unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null
@@ -67,6 +72,13 @@ __host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain
 // mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
+// K slices for a split-K launch of `tiles` output tiles over `kmain` K steps:
+// enough workgroups for `want` (every slice non-empty); 1 = no split
+int xgemm_splitk_for(int tiles, int kmain, int want);
+// out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
+// split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)
+hipError_t launch_xgemm_splitk_reduce(const float* part, int ksplit, int M, int Nc, const float* bias, int act,
+                                      float* out, int ldo, hipStream_t st);
 
 // Host packing of the weights of up to two segments (segment s: fp32
 // W_s[n][tap * cin_s + c], row stride ldw_s) into the tile layout above,

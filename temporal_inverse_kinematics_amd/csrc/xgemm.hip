@@ -119,14 +119,17 @@ struct XCfg {
     static constexpr int NIBW = (NIB_TOT + NW - 1) / NW;   // B DMA instructions per wave per stage (at most)
     static constexpr int RT = EPI == EPI_GRAPH ? BM / 17 * 17 : BM;   // valid rows per tile (whole frames for the mix)
     static constexpr int LDCG = BN + 4;
-    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : 0;   // C tile + bias2 slice
+    // C tile (+ the bias2 slice for the graph mix)
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : BM * LDCG * 4;
     static constexpr int SMEM = RING > CT ? RING : CT;
     static constexpr int WG_PER_CU = NW == 8 ? 1 : 2;
     static_assert(NIA * 1024 * NW == ABYTES && NIA * 8 == RW, "A DMA split");
     static_assert(SMEM * WG_PER_CU <= 160 * 1024, "LDS");
 };
 
-template <int BN, int EPI, int NW_>
+// SK: a split-K launch (XArgs::ksplit > 1; its own instantiation, so the
+// profiler tells it from the backbone's EPI_BIAS launches)
+template <int BN, int EPI, int NW_, bool SK>
 __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs a) {
     using C = XCfg<BN, EPI, NW_>;
     constexpr int NW = C::NW, NT = C::NT, FM = C::FM, FN = C::FN, NIA = C::NIA, NSA = C::NSA, NSB = C::NSB,
@@ -176,10 +179,18 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         a_n[j] = q / a.tout;
         a_t[j] = q - a_n[j] * a.tout;
     }
-    const int kmain = xgemm_kmain(a);   // K steps with weight tiles; the identity steps follow
-    const int K = a.ksteps;
+    // K steps with weight tiles (the identity steps follow); a split-K slice
+    // runs packed steps kb .. kb + kmain of its single kt-1 segment
+    const int kall = xgemm_kmain(a);
+    int kb = 0, kmain = kall;
+    if (SK) {
+        const int kper = (kall + a.ksplit - 1) / a.ksplit;
+        kb = blockIdx.z * kper;
+        kmain = min(kper, kall - kb);
+    }
+    const int K = SK ? kmain : a.ksteps;
     // B DMA: a stage's B image is one contiguous packed block; instruction q (of NIB_TOT) copies 1 KB
-    const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kmain * C::BBYTES));
+    const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kall * C::BBYTES));
     const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage (NIBW or NIBW - 1)
 
     // The A cursor walks (segment, tap, 32-channel block); segment slot 0 =
@@ -193,7 +204,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         (unsigned long long)((a.seg[0].cin >> 5) | (a.seg[0].kt << 8)) |
         ((unsigned long long)(two ? (a.seg[1].cin >> 5) | (a.seg[1].kt << 8) : (a.idn.cin >> 5) | (a.idn.kt << 8)) << 16) |
         ((unsigned long long)((a.idn.cin >> 5) | (a.idn.kt << 8)) << 32);
-    int ca_seg = 0, ca_tap = 0, ca_blk = 0, ca_k = 0, cb_k = 0;
+    int ca_seg = 0, ca_tap = 0, ca_blk = kb, ca_k = 0, cb_k = 0;
     auto advance_a = [&]() __attribute__((always_inline)) {
         const unsigned f = (unsigned)(nbkt >> (16 * ca_seg));
         ++ca_k;
@@ -233,7 +244,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     };
     auto issue_b = [&]() __attribute__((always_inline)) {   // weight step cb_k (main steps only)
         unsigned char* B = b_slot(cb_k % NSB);
-        const int soB = __builtin_amdgcn_readfirstlane((ntile * kmain + cb_k) * C::BBYTES);
+        const int soB = __builtin_amdgcn_readfirstlane((ntile * kall + kb + cb_k) * C::BBYTES);
         if (!(a.tune & 2))
 #pragma unroll
             for (int q = 0; q < C::NIBW; ++q)
@@ -403,9 +414,65 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     };
 
     if constexpr (TR) {
+        const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
+        float* const outp = SK ? a.out + (size_t)blockIdx.z * a.M * a.ldo : a.out;
+        if (a.epi_lds) {
+            // ---- EPI_BIAS through LDS: each wave stages its own 32 rows (no barrier
+            // between its writes and reads) and stores them row-major, so every
+            // store instruction writes whole 128-B lines (RPI rows x BN x 4 B)
+            // instead of 16 half lines (one 64-B piece per row)
+            constexpr int LDC = BN + 4, LPR = BN / 4, RPI = 64 / LPR, NQ = RW / RPI;
+            constexpr int NQR = BN == 64 ? NQ : 1;
+            float* Cs = reinterpret_cast<float*>(smem);
+            const int cl = 4 * (lane % LPR), col = n0 + cl, rsub = lane / LPR;
+            const bool cok = col + 3 < a.Nc;
+            // global operands before the first store (vmcnt counts loads and stores in order)
+            const f32x4 bv = a.bias && cok ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+            float rw[4][4];
+            f32x4 xr[NQR];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) rw[e][c] = BN == 64 && a.rx && c < a.rxc && col + e < a.Nc ? a.rw[(col + e) * a.rxc + c] : 0.f;
+#pragma unroll
+            for (int q = 0; q < NQR; ++q) {
+                const int lr = wave * RW + q * RPI + rsub;
+                xr[q] = BN == 64 && a.rx && lr < RT && r0 + lr < a.M ? *reinterpret_cast<const f32x4*>(a.rx + (size_t)(r0 + lr) * 4)
+                                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            __syncthreads();   // every wave done reading the ring (the B slots are shared)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    *reinterpret_cast<f32x4*>(Cs + (wave * RW + 16 * i + (lane & 15)) * LDC + 16 * j + 4 * g) = acc[i][j];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int lr = wave * RW + q * RPI + rsub;
+                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + cl) + bv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (BN == 64 && a.rx) v[e] += xr[q % NQR][0] * rw[e][0] + xr[q % NQR][1] * rw[e][1] + xr[q % NQR][2] * rw[e][2] + xr[q % NQR][3] * rw[e][3];
+                    v[e] = v[e] > 0.f ? v[e] : slope * v[e];
+                }
+                if (lr < RT && r0 + lr < a.M) {
+                    if (cok) {
+                        *reinterpret_cast<f32x4*>(outp + (size_t)(r0 + lr) * a.ldo + col) = v;
+                    } else {
+                        for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
+                            float t = *(Cs + lr * LDC + cl + e) + (a.bias ? a.bias[col + e] : 0.f);
+                            if (a.rx)
+                                for (int c = 0; c < a.rxc; ++c) t = fmaf(xr[q % NQR][c], a.rw[(col + e) * a.rxc + c], t);
+                            outp[(size_t)(r0 + lr) * a.ldo + col + e] = t > 0.f ? t : slope * t;
+                        }
+                    }
+                }
+            }
+            trace_out();
+            return;
+        }
         // ---- EPI_BIAS from registers: acc[i][j] lane l = row wave*32 + 16i + (l & 15),
         // channels n0 + 16j + 4(l >> 4) .. +3: float4 operands and stores, no LDS
-        const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
         int rows[FM];
         bool rok[FM];
 #pragma unroll
@@ -459,7 +526,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                         v[e] += xr[i][0] * rw[e][0] + xr[i][1] * rw[e][1] + xr[i][2] * rw[e][2] + xr[i][3] * rw[e][3];
                         v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                     }
-                    if (rok[i]) *reinterpret_cast<f32x4*>(a.out + (size_t)rows[i] * a.ldo + col) = v;
+                    if (rok[i]) *reinterpret_cast<f32x4*>(outp + (size_t)rows[i] * a.ldo + col) = v;
                 }
             } else {
 #pragma unroll
@@ -470,7 +537,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                         if (a.rx)
                             for (int c = 0; c < a.rxc; ++c) t = fmaf(xr[i][c], a.rw[(col + e) * a.rxc + c], t);
                         t = t > 0.f ? t : slope * t;
-                        a.out[(size_t)rows[i] * a.ldo + col + e] = t;
+                        outp[(size_t)rows[i] * a.ldo + col + e] = t;
                     }
                 }
             }
@@ -547,10 +614,21 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const int nw = a.nw == 8 ? 8 : 4, rt = xgemm_tile_rows(epi, nw);
     if (a.nw != 0 && a.nw != 4 && a.nw != 8) return hipErrorInvalidValue;
-    const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn), blk(64 * nw);
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    if (ks > 1) {   // one kt-1 segment, raw partials, every slice non-empty
+        const int kall = xgemm_kmain(a), kper = (kall + ks - 1) / ks;
+        if (epi != EPI_BIAS || a.nseg != 1 || a.seg[0].kt != 1 || a.idn.src || a.rx || a.bias || a.act != ACT_NONE ||
+            (ks - 1) * kper >= kall || a.trace)
+            return hipErrorInvalidValue;
+    }
+    const dim3 grid((a.M + rt - 1) / rt, (a.Nc + bn - 1) / bn, ks), blk(64 * nw);
     (void)hipGetLastError();
-#define XL(BN_, EPI_, NW__) hipLaunchKernelGGL((xgemm_kernel<BN_, EPI_, NW__>), grid, blk, 0, st, a)
-    if (nw == 4) {
+#define XL(BN_, EPI_, NW__) hipLaunchKernelGGL((xgemm_kernel<BN_, EPI_, NW__, false>), grid, blk, 0, st, a)
+    if (ks > 1) {
+        if (bn == 128 && nw == 4) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 4, true>), grid, blk, 0, st, a);
+        else if (bn == 128) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 8, true>), grid, blk, 0, st, a);
+        else return hipErrorInvalidValue;
+    } else if (nw == 4) {
         if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 4); else XL(128, EPI_GRAPH, 4); }
         else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 4); else XL(64, EPI_GRAPH, 4); }
     } else {
@@ -558,6 +636,43 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
         else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 8); else XL(64, EPI_GRAPH, 8); }
     }
 #undef XL
+    return hipGetLastError();
+}
+
+int xgemm_splitk_for(int tiles, int kmain, int want) {
+    int ks = std::max(1, std::min((want + tiles - 1) / std::max(1, tiles), kmain / 8));
+    if (ks <= 1) return 1;
+    const int kper = (kmain + ks - 1) / ks;
+    return (kmain + kper - 1) / kper;   // every slice non-empty
+}
+
+__global__ __launch_bounds__(256) void xgemm_splitk_reduce_kernel(const float* __restrict__ part, int ksplit, int M,
+                                                                  int Nc, const float* __restrict__ bias, float slope,
+                                                                  float* __restrict__ out, int ldo) {
+    const int c4 = Nc / 4;
+    const long long n = (long long)M * c4, plane = (long long)M * Nc;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int r = (int)(i / c4), c = 4 * (int)(i - (long long)r * c4);
+        const float* p = part + (size_t)r * Nc + c;
+        f32x4 v = bias ? *reinterpret_cast<const f32x4*>(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 s = *reinterpret_cast<const f32x4*>(p);
+        for (int z = 1; z < ksplit; ++z) s += *reinterpret_cast<const f32x4*>(p + z * plane);
+        v = s + v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : slope * v[e];
+        *reinterpret_cast<f32x4*>(out + (size_t)r * ldo + c) = v;
+    }
+}
+
+hipError_t launch_xgemm_splitk_reduce(const float* part, int ksplit, int M, int Nc, const float* bias, int act,
+                                      float* out, int ldo, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!part || !out || ksplit < 1 || Nc % 4 || ldo % 4) return hipErrorInvalidValue;
+    const float slope = act == ACT_RELU ? 0.f : (act == ACT_LEAKY ? 0.01f : 1.f);
+    const long long n = (long long)M * (Nc / 4);
+    const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(xgemm_splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, part, ksplit, M, Nc, bias, slope, out, ldo);
     return hipGetLastError();
 }
 

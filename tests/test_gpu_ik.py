@@ -243,20 +243,16 @@ def test_fused_gcn_epilogue_bitwise():
             assert torch.equal(fused(x)["poses"], plain(x)["poses"]), (n, T)
 
 
-def test_two_stream_split_bitwise():
-    """Large f16x3 batches run as two halves on two HIP streams (second
-    workspace, fork/join events): poses bit-identical to the one-stream run,
-    including an odd batch and one the DMA sub-batching also splits."""
-    import os
+@pytest.mark.parametrize("precision,lag", [("f16x3", None), ("bf16x3", None), ("bf16x3", 1), ("bf16x3", 4)])
+def test_two_stream_split_bitwise(precision, lag):
+    """Large batches run as two parts on two HIP streams (second workspace,
+    fork/join events): poses bit-identical to the one-stream run, including
+    an odd batch and one the DMA sub-batching also splits. bf16x3 (xgemm
+    path): also with part 1 starting after part 0's first / fourth launch
+    (TIK_SPLIT_LAG), so the parts' graph and temporal launches interleave."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    from temporal_inverse_kinematics_amd.inference import synthetic_model
-    split = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
-    os.environ["TIK_SPLIT"] = "0"
-    try:
-        one = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
-        one.tik_handle()
-    finally:
-        del os.environ["TIK_SPLIT"]
+    split = _model_with_env(precision, **({"TIK_SPLIT_LAG": lag} if lag else {}))
+    one = _model_with_env(precision, TIK_SPLIT=0)
     for n in (1024, 1001, 513):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 1)).cuda()
         with torch.no_grad():
@@ -297,14 +293,14 @@ def test_two_stream_split_with_dma_chunks_bitwise():
             assert torch.equal(chunked(x)["poses"], one(x)["poses"]), n
 
 
-def test_two_stream_split_repeated_bitwise():
+@pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
+def test_two_stream_split_repeated_bitwise(precision):
     """the default two-stream split path, repeated 40
     times back to back (the halves overlap differently on every run), stays
     bit-identical to the one-stream result."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    from temporal_inverse_kinematics_amd.inference import synthetic_model
-    split = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
-    one = _model_with_env(TIK_SPLIT=0)
+    split = _model_with_env(precision)
+    one = _model_with_env(precision, TIK_SPLIT=0)
     x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=11)).cuda()
     with torch.no_grad():
         ref = one(x)["poses"].clone()
@@ -435,3 +431,21 @@ def test_moveai_to_coco_device_bit_exact():
     assert np.array_equal(got, k["coco_seq"])
     with pytest.raises(RuntimeError):
         moveai3d_to_coco_device(torch.zeros(3, 22, 3), k["moveai_names"].tolist())
+
+
+@pytest.mark.parametrize("n", [1024, 37])
+def test_xgemm_head_splitk_matches_cgemm_head(n):
+    """The bf16x3 head (pose_regressor.0 on xgemm with its K loop split over
+    enough workgroups to fill the chip, slices summed in a fixed order) agrees
+    with the register-staged split-K head (TIK_XHEAD_WGS=0) to fp32 rounding,
+    and is run-to-run bit-identical."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    xh = _model_with_env("bf16x3", TIK_SPLIT=0)
+    ch = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XHEAD_WGS=0)
+    x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 3)).cuda()
+    with torch.no_grad():
+        a = xh(x)["poses"].clone()
+        b = ch(x)["poses"]
+        assert torch.equal(xh(x)["poses"], a)
+    scale = float(b.abs().max())
+    assert float((a - b).abs().max()) <= 2e-6 * max(1.0, scale), float((a - b).abs().max())

@@ -39,7 +39,9 @@ def main():
     gemm_flops = 2.0 * B * 3 * V * 507 + 2.0 * B * V * 12 * 55 + 18.0 * B * V
     out = {"metric": "SMPL-X FK+LBS bodies/sec", "value": round(B / (ms / 1e3), 1), "unit": "bodies/s",
            "n_gpus": 1, "ms_per_step": round(ms, 4),
-           "dtype": "f32 via 3xf16-split MFMA, fp32 accumulate" if m.precision != "fp32" else "f32 (fp32 MFMA)", "config": {"workload": f"SMPL-X 55-joint FK + {V}-vertex LBS + 144 joints, batch={B}"},
+           "dtype": {"bf16x3": "f32 via bf16x3 (3 bf16 planes, 6 MFMA products, fp32 accumulate; fp32 exponent range)",
+                     "f16x3": "f32 via f16x3 (3 MFMA products; f16 range, narrower than fp32)",
+                     "fp32": "f32 (exact fp32 MFMA)"}.get(m.precision, m.precision), "config": {"workload": f"SMPL-X 55-joint FK + {V}-vertex LBS + 144 joints, batch={B}"},
            "gemm_tflops": round(gemm_flops / (ms / 1e3) / 1e12, 2), "mflop_per_body": round(gemm_flops / B / 1e6, 2),
            "bytes_out_per_body": (V * 3 + 144 * 3) * 4}
     from oracle import smplx_lbs as sl

@@ -128,6 +128,11 @@ hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, co
     return e;
 }
 
+// desync experiment on the xgemm kernels (XArgs::stagger), TIK_XSTAGGER=<n>; 0 in production
+static int xstagger() {
+    static const int v = [] { const char* e = getenv("TIK_XSTAGGER"); return e ? atoi(e) : 0; }();
+    return v;
+}
 // tuning experiments on the xgemm kernels (XArgs::tune), TIK_XTUNE=<bits>; 0 in production
 int xtune() {
     static const int t = getenv("TIK_XTUNE") ? atoi(getenv("TIK_XTUNE")) : 0;
@@ -228,7 +233,7 @@ struct Layer {
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
-    int xepi = 1;           // xgemm EPI_BIAS epilogue through LDS, whole-line stores (TIK_XEPI=0: from registers)
+    int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -394,7 +399,7 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune(); g.nw = xnw;
+            g.tune = xtune(); g.nw = xnw; g.stagger = xstagger();
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
@@ -421,7 +426,7 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi;
+        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger();
         const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
@@ -719,7 +724,7 @@ struct tik_model {
     SplitW3 s30, s33;
     SBW sb0, sb3;
     DevHBuf xh0;                   // bf16x3 tiles of pose_regressor.0 for xgemm.hip (feat % 32 == 0)
-    int xhead_wgs = 512;           // xgemm head: split K until this many workgroups (TIK_XHEAD_WGS; 0: the cgemm head)
+    int xhead_ks = 4;              // xgemm head: K slices, fixed so a window's poses do not depend on the batch size (TIK_XHEAD_KS; 0: the cgemm head)
     int prec = 1;
     // ws[0]: the handle's workspace (z, z2: ping-pong for the fused T+G launches);
     // ws[1] + a private stream: large f16x3 batches run as two halves on two
@@ -896,7 +901,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_XNW"))
         for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("TIK_XEPI"))
-        for (auto& L : md->layers) L.xepi = e[0] != '0';
+        for (auto& L : md->layers) L.xepi = atoi(e);
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT_LAG")) md->split_lag = std::max(0, atoi(e));
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
@@ -915,7 +920,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         delete md;
         return rc;
     }
-    if (const char* e = getenv("TIK_XHEAD_WGS")) md->xhead_wgs = atoi(e);
+    if (const char* e = getenv("TIK_XHEAD_KS")) md->xhead_ks = std::min(8, atoi(e));
     if (md->feat % 32 == 0) {
         const tik::XPackSeg h{W0->v.data(), md->feat, 1, md->feat};
         if ((rc = md->xh0.upload(tik::xgemm_pack(&h, 1, md->hidden, 128)))) { delete md; return rc; }
@@ -1212,7 +1217,7 @@ static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses
     return TIK_OK;
 }
 
-static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st);
+static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st, int ks = 0);
 
 // Head on fp32 features with split-K (few rows: the K = 4352 loop spread over
 // workgroups instead of run serially by the handful of row tiles).
@@ -1232,12 +1237,13 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
 }
 
 // the head's second layer (hidden -> pose_dim, pose_trainer.py:92) with split-K
-static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st) {
+// (ks > 0: that many K slices whatever the row count)
+static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st, int ks) {
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
     p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->s33, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
-    p.ksplit = tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
+    p.ksplit = ks > 0 ? ks : tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
     p.partial = part;
     {
         ProfScope pr("H64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
@@ -1248,20 +1254,21 @@ static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses,
 }
 
 // Head of the bf16x3 path: pose_regressor.0 (feat -> hidden, LeakyReLU,
-// pose_trainer.py:89-91) on xgemm.hip, its K = feat loop split over enough
-// workgroups to fill the chip (the frames are few: 4096 rows at B = 1024) and
+// pose_trainer.py:89-91) on xgemm.hip, its K = feat loop split into a fixed
+// number of slices (the frames are few: 4096 rows at B = 1024, 128 tiles) and
 // the slices summed in a fixed order by the reduce kernel (+ bias, LeakyReLU);
 // then pose_regressor.3 with split-K as head_splitk.
 static int head_x(tik_model_t m, const float* f, int rows, float* poses, const WsPtrs& w, hipStream_t st) {
-    if (!m->xh0.p || m->xhead_wgs <= 0) return head_splitk(m, f, rows, poses, w.hid, w.part, st);
+    if (!m->xh0.p || m->xhead_ks <= 0) return head_splitk(m, f, rows, poses, w.hid, w.part, st);
     tik::XArgs h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
     h.seg[0] = tik::XSeg{f, m->feat, m->feat, 1, 1, 0, rows, rows};
     h.nseg = 1; h.wp = m->xh0.p; h.ksteps = tik::xgemm_ksteps(h);
-    h.nw = m->layers.front().xnw; h.epi_lds = m->layers.front().xepi;
-    const int tiles = ((rows + tik::xgemm_tile_rows(tik::EPI_BIAS, h.nw) - 1) / tik::xgemm_tile_rows(tik::EPI_BIAS, h.nw)) *
-                      ((m->hidden + 127) / 128);
-    h.ksplit = std::min(8, tik::xgemm_splitk_for(tiles, h.ksteps, m->xhead_wgs));
+    h.nw = m->layers.front().xnw; h.epi_lds = m->layers.front().xepi != 0;
+    {   // K slices: the fixed count (4: 512 workgroups at 4096 rows), each non-empty
+        const int kper = (h.ksteps + m->xhead_ks - 1) / m->xhead_ks;
+        h.ksplit = (h.ksteps + kper - 1) / kper;
+    }
     if (h.ksplit > 1) {
         h.out = w.part; h.act = tik::ACT_NONE;
     } else {
@@ -1278,7 +1285,9 @@ static int head_x(tik_model_t m, const float* f, int rows, float* poses, const W
         HIP_TRY(tik::launch_xgemm_splitk_reduce(w.part, h.ksplit, rows, m->hidden, m->b0.p, tik::ACT_LEAKY, w.hid,
                                                 m->hidden, st));
     }
-    return head3_splitk(m, w.hid, rows, poses, w.part, st);
+    // pose_regressor.3: a fixed K split too (4 slices of 128), so no row's
+    // arithmetic depends on the batch size
+    return head3_splitk(m, w.hid, rows, poses, w.part, st, std::min(4, std::max(1, m->hidden / 128)));
 }
 
 }  // extern "C"

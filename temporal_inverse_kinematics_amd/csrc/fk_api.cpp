@@ -7,7 +7,8 @@
 //   tgemm (TG_128x128)  v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
 //   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// (f16x3 on split-block operands; fp32 and bf16x3 run both GEMMs on cgemm.hip)
+// (f16x3 on split-block operands; bf16x3: the blend shapes on xgemm.hip and
+// the skinning on cgemm.hip; fp32 both on cgemm.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,6 +20,7 @@
 #include "common.h"
 #include "fk.h"
 #include "cgemm3.h"
+#include "xgemm.h"
 
 using namespace tik_host;
 
@@ -36,6 +38,7 @@ struct tik_fk {
     SplitW sPT, sWT;   // f16 hi/lo planes (fp32 path's register-staged GEMMs)
     SplitW3 s3PT, s3WT;   // bf16 planes p0+p1+p2 (bf16x3 register-staged GEMMs)
     SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
+    DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
     DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra, depth;
@@ -175,6 +178,14 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         delete fk;
         return rc;
     }
+    const char* xe = getenv("TIK_FK_XGEMM");
+    if (!(xe && xe[0] == '0')) {
+        const tik::XPackSeg ps{PT.data(), KP, 1, KP};
+        if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128)))) {
+            delete fk;
+            return rc;
+        }
+    }
     if (fk->contour && ((rc = fk->dyn_faces.upload(hdf)) || (rc = fk->dyn_bary.upload(db->v)))) {
         delete fk;
         return rc;
@@ -255,6 +266,15 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         s.trash = fk->trash.p;
         HIP_TRY(tik::launch_fk_skin(s, st));
     } else {
+        if (fk->prec == tik::PREC_BF16X3 && fk->xPT.p) {
+            // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA)
+            tik::XArgs g{};
+            g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
+            g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
+            g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
+            g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
+            HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, st));
+        } else {
         tik::CgemmArgs g{};   // v_posed = feat . P
         g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
         g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
@@ -262,6 +282,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         for (int i = 0; i < 3; ++i) g.seg[0].wb[i] = fk->s3PT.p[i].p;
         g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
         HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
+        }
 
         tik::CgemmArgs s{};   // skinning + vertex transform
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;

@@ -54,8 +54,10 @@ struct XArgs {
     // blockIdx.z = k slice; slice z writes its raw partial sums to
     // out + z * M * ldo, and xgemm_splitk_reduce finishes (0 or 1: no split)
     int ksplit;
+    int idn_epi;  // with epi_lds: the identity residual added in the epilogue from row-major loads (no K steps)
     int epi_lds;  // EPI_BIAS: stage the C tile through LDS for whole-line row-major stores (else float4 stores from registers)
     int nw;     // waves per workgroup: 4 (or 0: two 128-row workgroups per CU) or 8 (one 256-row workgroup)
+    int stagger;   // experiment (TIK_XSTAGGER): the second half of the first 2 x 256 workgroups sleeps stagger x 8k cycles first
     int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA, 8 skip the split
     unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null
 };
@@ -72,9 +74,6 @@ __host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain
 // mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
-// K slices for a split-K launch of `tiles` output tiles over `kmain` K steps:
-// enough workgroups for `want` (every slice non-empty); 1 = no split
-int xgemm_splitk_for(int tiles, int kmain, int want);
 // out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)
 hipError_t launch_xgemm_splitk_reduce(const float* part, int ksplit, int M, int Nc, const float* bias, int act,

@@ -150,6 +150,11 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         r0 = (swz / gridDim.y) * RT;
         ntile = swz % gridDim.y;
     }
+    if (a.stagger > 0) {   // desynchronise the two workgroups per CU (experiment)
+        const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+        if (bid >= 256 && bid < 512)
+            for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     const int n0 = ntile * BN;
     const int V = a.V;
     // EPI_GRAPH: this tile's bias2[17][n0 .. n0 + BN) slice, loaded now so its
@@ -188,7 +193,9 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         kb = blockIdx.z * kper;
         kmain = min(kper, kall - kb);
     }
-    const int K = SK ? kmain : a.ksteps;
+    // the identity residual read in the LDS epilogue (row-major whole lines) instead of as K steps
+    const bool idn_epi = TR && a.epi_lds && a.idn_epi && a.idn.src;
+    const int K = SK || idn_epi ? kmain : a.ksteps;
     // B DMA: a stage's B image is one contiguous packed block; instruction q (of NIB_TOT) copies 1 KB
     const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kall * C::BBYTES));
     const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage (NIBW or NIBW - 1)
@@ -440,6 +447,17 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 xr[q] = BN == 64 && a.rx && lr < RT && r0 + lr < a.M ? *reinterpret_cast<const f32x4*>(a.rx + (size_t)(r0 + lr) * 4)
                                                                       : f32x4{0.f, 0.f, 0.f, 0.f};
             }
+            constexpr int NQI = TR ? NQ : 1;
+            f32x4 xi[NQI];
+            if (idn_epi) {   // the identity residual rows (block input = output row, same channels)
+#pragma unroll
+                for (int q = 0; q < NQI; ++q) {
+                    const int lr = wave * RW + q * RPI + rsub;
+                    xi[q] = cok && lr < RT && r0 + lr < a.M
+                                ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.idn.src + (size_t)(r0 + lr) * a.idn.ld + col))
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
             __syncthreads();   // every wave done reading the ring (the B slots are shared)
 #pragma unroll
             for (int i = 0; i < FM; ++i)
@@ -449,7 +467,9 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int lr = wave * RW + q * RPI + rsub;
-                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + cl) + bv;
+                f32x4 v = *reinterpret_cast<const f32x4*>(Cs + lr * LDC + cl);
+                if (idn_epi) v += xi[q % NQI];   // same order as the K-step adds: (acc + x) + bias
+                v += bv;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (BN == 64 && a.rx) v[e] += xr[q % NQR][0] * rw[e][0] + xr[q % NQR][1] * rw[e][1] + xr[q % NQR][2] * rw[e][2] + xr[q % NQR][3] * rw[e][3];
@@ -637,13 +657,6 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     }
 #undef XL
     return hipGetLastError();
-}
-
-int xgemm_splitk_for(int tiles, int kmain, int want) {
-    int ks = std::max(1, std::min((want + tiles - 1) / std::max(1, tiles), kmain / 8));
-    if (ks <= 1) return 1;
-    const int kper = (kmain + ks - 1) / ks;
-    return (kmain + kper - 1) / kper;   // every slice non-empty
 }
 
 __global__ __launch_bounds__(256) void xgemm_splitk_reduce_kernel(const float* __restrict__ part, int ksplit, int M,

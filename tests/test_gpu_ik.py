@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xnw8", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
+@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
                                                  "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
                                                  "f16x3-dmahead"])
 def model(request):
@@ -43,7 +43,10 @@ def model(request):
                # xgemm in sub-batches of at most 3 windows (the 2 GiB-per-tensor split)
                "xchunk": {"TIK_DMA_CHUNK": "3"},
                # xgemm with one 256-row, 8-wave workgroup per CU (default: two 128-row ones)
-               "xnw8": {"TIK_XNW": "8"}}.get(path, {"TIK_GEMM_PATH": path})
+               "xnw8": {"TIK_XNW": "8"},
+               # xgemm temporal-conv epilogue from registers (half-line stores), and through LDS
+               # with the identity residual as extra K steps (default: loaded in the epilogue)
+               "xepi0": {"TIK_XEPI": "0"}, "xepi1": {"TIK_XEPI": "1"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created
@@ -436,12 +439,12 @@ def test_moveai_to_coco_device_bit_exact():
 @pytest.mark.parametrize("n", [1024, 37])
 def test_xgemm_head_splitk_matches_cgemm_head(n):
     """The bf16x3 head (pose_regressor.0 on xgemm with its K loop split over
-    enough workgroups to fill the chip, slices summed in a fixed order) agrees
-    with the register-staged split-K head (TIK_XHEAD_WGS=0) to fp32 rounding,
-    and is run-to-run bit-identical."""
+    a fixed number of K slices summed in a fixed order) agrees with the
+    register-staged split-K head (TIK_XHEAD_KS=0) to fp32 rounding, and is
+    run-to-run bit-identical."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     xh = _model_with_env("bf16x3", TIK_SPLIT=0)
-    ch = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XHEAD_WGS=0)
+    ch = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XHEAD_KS=0)
     x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 3)).cuda()
     with torch.no_grad():
         a = xh(x)["poses"].clone()
@@ -449,3 +452,37 @@ def test_xgemm_head_splitk_matches_cgemm_head(n):
         assert torch.equal(xh(x)["poses"], a)
     scale = float(b.abs().max())
     assert float((a - b).abs().max()) <= 2e-6 * max(1.0, scale), float((a - b).abs().max())
+
+
+def test_xgemm_epilogue_variants():
+    """The xgemm temporal-conv epilogues: through LDS (TIK_XEPI=1, default)
+    and through LDS with the identity rows loaded in the epilogue instead of
+    as K steps (2) do the same fp32 operations in the same order ((acc +
+    identity residual) + bias, activation): bit-identical poses. From
+    registers (0) the compiler contracts layer 0's residual-conv terms into
+    FMAs differently: equal to fp32 rounding."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    ms = [_model_with_env("bf16x3", TIK_SPLIT=0, TIK_XEPI=e) for e in (0, 1, 2)]
+    for n in (1024, 37):
+        x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 5)).cuda()
+        with torch.no_grad():
+            ys = [m(x)["poses"].clone() for m in ms]
+        assert torch.equal(ys[1], ys[2]), n
+        assert float((ys[0] - ys[1]).abs().max()) < 1e-5, n
+
+
+def test_bf16x3_batch_invariant_bitwise():
+    """On the default bf16x3 path every output row is computed with the same
+    operations in the same order whatever the batch (row-local GEMM tiles, a
+    fixed K partition of the head): windows solved inside a 1024-window batch
+    (two streams), inside a 37-window batch and alone are bit-identical."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    m = synthetic_model(win_size=64, device="cuda", precision="bf16x3").regressor
+    x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=21)).cuda()
+    with torch.no_grad():
+        full = m(x)["poses"].clone()
+        part = m(x[:37])["poses"].clone()
+        assert torch.equal(part, full[:37])
+        for i in (0, 36, 511, 1023):
+            assert torch.equal(m(x[i:i + 1])["poses"], full[i:i + 1]), i

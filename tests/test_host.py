@@ -139,6 +139,7 @@ def test_bench_kernel_symbols_match_pmc_profile():
     tags = [os.path.basename(p)[:7] for p in glob.glob(os.path.join(repo, "profiles", "r*_v*_pmc_traffic.json"))]
     assert max(tags, key=lambda s: (int(s[1:3]), int(s.split("_v")[1].rstrip("_")))) in os.path.basename(newest)
     kernels = json.load(open(newest))["kernels"]
-    for label in ("TW_128", "GP_128", "GP_256", "TG3_128x128", "T3_128x128", "B3_64", "B0_64", "G3_272x128", "H3_64x64"):
-        traffic, src = bench._pmc_traffic(newest, label, "f16x3")
-        assert traffic is not None and traffic > 0, (label, bench.KERNEL_SYMBOLS.get(label), list(kernels))
+    # the default (bf16x3) path's launches
+    for label in ("XT128", "XG128", "XT64", "XG64", "XH128", "XR"):
+        traffic, src = bench._pmc_traffic(newest, label, "bf16x3")
+        assert traffic is not None and traffic > 0, (label, bench.kernel_symbol(label, "bf16x3"), list(kernels))

@@ -41,6 +41,8 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> st
     if not force and not _needs_rebuild(srcs, LIB):
         return LIB
     opt = ["-O0", "-g"] if debug else ["-O3"]
+    # diagnostic builds: e.g. TIK_HIPCC_FLAGS="-DTIK_XTRACE" (xgemm phase stamps), "-DTIK_XTUNE"
+    opt += os.environ.get("TIK_HIPCC_FLAGS", "").split()
     common = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
               f"-I{os.path.join(REPO, 'include')}", *opt]
 

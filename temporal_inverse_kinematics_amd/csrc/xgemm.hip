@@ -38,6 +38,7 @@
 //    (st_gcn_aaai18.py:178-179).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "cgemm.h"
 #include "cgemm3_dev.h"
@@ -139,7 +140,18 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // phase stamps only in a -DTIK_XTRACE build: a runtime check puts a scalar
+    // branch around every stamp of the K loop
+#ifdef TIK_XTRACE
     const bool tr = a.trace != nullptr;
+#else
+    constexpr bool tr = false;
+#endif
+#ifdef TIK_XTUNE
+    const int tune = a.tune;
+#else
+    constexpr int tune = 0;   // experiment bits (XArgs::tune) only in a -DTIK_XTUNE build
+#endif
     unsigned long long t0 = tr ? __builtin_amdgcn_s_memtime() : 0, t_bar = 0, t_vm = 0, t1 = 0, t2 = 0, t3 = 0;
     int r0, ntile;
     {   // XCD-aware tile order: consecutive workgroup ids go to different XCDs,
@@ -242,7 +254,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         prepare();
         unsigned char* A = a_slot(ca_k % NSA);
         const int soA = __builtin_amdgcn_readfirstlane(ca_blk * 128);
-        if (!(a.tune & 1))
+        if (!(tune & 1))
 #pragma unroll
             for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
         const int seg = ca_seg, tap = ca_tap;
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     auto issue_b = [&]() __attribute__((always_inline)) {   // weight step cb_k (main steps only)
         unsigned char* B = b_slot(cb_k % NSB);
         const int soB = __builtin_amdgcn_readfirstlane((ntile * kall + kb + cb_k) * C::BBYTES);
-        if (!(a.tune & 2))
+        if (!(tune & 2))
 #pragma unroll
             for (int q = 0; q < C::NIBW; ++q)
                 if (q < C::NIBW - 1 || wave + q * NW < C::NIB_TOT)
@@ -264,7 +276,8 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     auto nA = [&](int k) __attribute__((always_inline)) { return k < K ? NIA : 0; };
     auto nB = [&](int k) __attribute__((always_inline)) { return k < kmain ? nbw : 0; };
     auto wait_steady = [&]() __attribute__((always_inline)) {   // NIA + this wave's full B share outstanding
-        if (nbw == C::NIBW) wait_vm<NIA + C::NIBW>();
+        if constexpr (C::NIB_TOT % NW == 0) wait_vm<NIA + C::NIBW>();   // every wave issues NIBW
+        else if (nbw == C::NIBW) wait_vm<NIA + C::NIBW>();
         else wait_vm<NIA + C::NIBW - 1>();
     };
 
@@ -312,22 +325,28 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     // reads and split into nxt interleaved between them (the loop below runs it
     // twice per iteration with the two register sets swapped: no copies)
     xbf16x8 d0[FM], d1[FM], d2[FM];
-    auto main_step = [&](int k, xbf16x8 (&u0)[FM], xbf16x8 (&u1)[FM], xbf16x8 (&u2)[FM], xbf16x8 (&v0)[FM],
+    // ST (steady, k + 2 < kmain: B(k+LB) and A(k+2) both exist): no conditions,
+    // compile-time waits; the last steps take the general path
+    auto main_step = [&](int k, auto steady, xbf16x8 (&u0)[FM], xbf16x8 (&u1)[FM], xbf16x8 (&u2)[FM], xbf16x8 (&v0)[FM],
                          xbf16x8 (&v1)[FM], xbf16x8 (&v2)[FM]) __attribute__((always_inline)) {
+        constexpr bool ST = decltype(steady)::value;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const unsigned long long tb0 = tr ? __builtin_amdgcn_s_memtime() : 0;
         __builtin_amdgcn_s_barrier();   // every wave's B(k) landed; every wave done reading B(k-1)
         if (tr) t_bar += __builtin_amdgcn_s_memtime() - tb0;
-        if (k + LB < kmain) issue_b();
-        if (k + 2 < K) issue_a();
+        if (ST || k + LB < kmain) issue_b();
+        if (ST || k + 2 < K) issue_a();
         // this wave's A(k+1) landed (B(k+LB), A(k+2) may still fly); past the last
         // step the read + split below run on a stale slot and are discarded
-        {
+        auto wait_a_next = [&]() __attribute__((always_inline)) {
             const unsigned long long tv0 = tr ? __builtin_amdgcn_s_memtime() : 0;
-            if (k + 2 < kmain) wait_steady();
+            if (ST || k + 2 < kmain) wait_steady();
             else wait_vm_dyn(nB(k + LB) + nA(k + 2));
             if (tr) t_vm += __builtin_amdgcn_s_memtime() - tv0;
-        }
+        };
+#ifndef TIK_XORDER
+        wait_a_next();
+#endif
         const unsigned char* B = b_slot(k % NSB) + boff;
         // Software pipeline inside the step: the A reads of step k+1 and the
         // first weight block's reads, then per column block j the next block's
@@ -336,9 +355,19 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         // between block j's MFMAs. sched_barriers keep the blocks in this order.
         xbf16x8 bb[2][3];
         __builtin_amdgcn_sched_barrier(0);
+#ifdef TIK_XORDER
+        // B(k) is ready at the barrier: its first block's reads go out before the
+        // wait for A(k+1), so they overlap that wait and the first MFMAs need not
+        // wait for the A reads
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bb[0][p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE);
+        wait_a_next();
+        read_a(k + 1, alo, ahi);
+#else
         read_a(k + 1, alo, ahi);
 #pragma unroll
         for (int p = 0; p < 3; ++p) bb[0][p] = *reinterpret_cast<const xbf16x8*>(B + p * C::PLANE);
+#endif
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -356,7 +385,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 mma(u0[i], b[1], acc[i][j]);
                 mma(u0[i], b[0], acc[i][j]);
             }
-            if (j < FM && !(a.tune & 8)) xsplit8(alo[j], ahi[j], v0[j], v1[j], v2[j]);
+            if (j < FM && !(tune & 8)) xsplit8(alo[j], ahi[j], v0[j], v1[j], v2[j]);
             // past the last block the remaining fragments' splits
             if (j == FN - 1)
 #pragma unroll
@@ -371,13 +400,21 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         }
         if constexpr (LB == 1) {   // B(k+1) landed before the next step's barrier (only A(k+2) younger)
             const unsigned long long tv0 = tr ? __builtin_amdgcn_s_memtime() : 0;
-            wait_vm_dyn(nA(k + 2));
+            if (ST) wait_vm<NIA>();
+            else wait_vm_dyn(nA(k + 2));
             if (tr) t_vm += __builtin_amdgcn_s_memtime() - tv0;
         }
     };
-    for (int k = 0; k < kmain; k += 2) {
-        main_step(k, c0, c1, c2, d0, d1, d2);
-        if (k + 1 < kmain) main_step(k + 1, d0, d1, d2, c0, c1, c2);
+    const std::true_type steady{};
+    const std::false_type general{};
+    int k = 0;
+    for (; k + 3 < kmain; k += 2) {   // both steps of the pair steady
+        main_step(k, steady, c0, c1, c2, d0, d1, d2);
+        main_step(k + 1, steady, d0, d1, d2, c0, c1, c2);
+    }
+    for (; k < kmain; k += 2) {
+        main_step(k, general, c0, c1, c2, d0, d1, d2);
+        if (k + 1 < kmain) main_step(k + 1, general, d0, d1, d2, c0, c1, c2);
     }
     if (tr) t2 = __builtin_amdgcn_s_memtime();
     // ---- identity residual steps (TR): acc += x, exact fp32 adds from this wave's rows

@@ -67,6 +67,8 @@ def kernel_symbol(label, precision):
         # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), waves per workgroup (TIK_XNW)>
         nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
         return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
+    if label[:2] == "XP" and label[2:] in ("64", "128"):
+        return f"tik::xgemm_pt_kernel<{label[2:]}>"
     if label == "XR":
         return "tik::xgemm_splitk_reduce_kernel"
     p = PREC_CODE[precision]

@@ -9,17 +9,19 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 TAG=$1; shift
 O=gpurun_out/ab_$TAG; mkdir -p $O
-lib() { [ "$1" = new ] && echo "" || echo "ab/libtik_$1.so"; }
+# a spec is NAME or NAME:VAR=VALUE[,VAR=VALUE] (the build, plus environment for its runs)
+lib() { local n=${1%%:*}; [ "$n" = new ] && echo "" || echo "ab/libtik_$n.so"; }
+envs() { [[ "$1" == *:* ]] && echo "${1#*:}" | tr ',' ' ' || echo "TIK_AB=1"; }
 if [ -n "${AB_TESTS:-}" ]; then
   for v in "$@"; do
     [ "$v" = base ] && continue
-    TIK_LIB=$(lib $v) timeout -k 10 300 python -u -m pytest tests/test_gpu_ik.py -m gpu -x -q --timeout 120 --timeout-method thread -k "${AB_K:-bf16x3}" > $O/pt_$v.log 2>&1; rc=$?
+    env $(envs $v) TIK_LIB=$(lib $v) timeout -k 10 300 python -u -m pytest tests/test_gpu_ik.py -m gpu -x -q --timeout 120 --timeout-method thread -k "${AB_K:-bf16x3}" > $O/pt_$v.log 2>&1; rc=$?
     echo "pytest $v: $(tail -1 $O/pt_$v.log)"; [ $rc -eq 0 ] || exit $rc
   done
 fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in "$@"; do
-    TIK_LIB=$(lib $v) timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-compare > $O/$v$r.json 2> $O/$v$r.err || exit 1
-    python -c "import json;d=json.load(open('$O/$v$r.json'));l=d['forward']['launches'];print('$v$r', d['value'], d['ms_per_step'], 'prof', d['profiled_ms_per_step'], ' '.join(f'{k}={v[\"avg_ms\"]}' for k,v in sorted(l.items()) if k.startswith('XT128') or k.startswith('XT64') or k.startswith('XG128.L3')))"
+    env $(envs $v) TIK_LIB=$(lib $v) timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-compare > $O/$v$r.json 2> $O/$v$r.err || exit 1
+    python -c "import json;d=json.load(open('$O/$v$r.json'));l=d['forward']['launches'];print('$v$r', d['value'], d['ms_per_step'], 'prof', d['profiled_ms_per_step'], ' '.join(f'{k}={v[\"avg_ms\"]}' for k,v in sorted(l.items()) if k.startswith('XT') or k.startswith('XP') or k.startswith('XG128.L3')))"
   done
 done

@@ -234,6 +234,9 @@ struct Layer {
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
+    int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; TIK_XPT bit mask of layers)
+    int ncu = 256;          // compute units (persistent grid size)
+    float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
 
     int build(const TensorMap& m, const std::string& pre, int cin_, int cout_, int stride_, int residual,
@@ -427,10 +430,16 @@ struct Layer {
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
         t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger();
-        const std::string lab = std::string(xt_bn == 128 ? "XT128.L" : "XT64.L") + std::to_string(index);
+        const bool pt = xpt && xtrash && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
+        const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
-        HIP_TRY(launch_xgemm_traced(t, xt_bn, tik::EPI_BIAS, st, lab.c_str()));
+        if (pt) {
+            t.trash = xtrash;
+            HIP_TRY(tik::launch_xgemm_pt(t, xt_bn, ncu, st));
+        } else {
+            HIP_TRY(launch_xgemm_traced(t, xt_bn, tik::EPI_BIAS, st, lab.c_str()));
+        }
         return TIK_OK;
     }
 
@@ -902,6 +911,16 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("TIK_XEPI"))
         for (auto& L : md->layers) L.xepi = atoi(e);
+    {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+            for (auto& L : md->layers) L.ncu = ncu;
+        const char* e = getenv("TIK_XPT");
+        for (auto& L : md->layers) {
+            L.xpt = e ? (atoi(e) >> L.index) & 1 : 0;   // TIK_XPT: bit l = layer l (255: all)
+            L.xtrash = reinterpret_cast<float*>(md->trash.p);
+        }
+    }
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
     if (const char* e = getenv("TIK_SPLIT_LAG")) md->split_lag = std::max(0, atoi(e));
     if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));

@@ -48,6 +48,7 @@ struct XArgs {
     const float* amix;          // EPI_GRAPH [V][V], A_eff[v][w]
     int mix_sparse;
     float* out;                 // fp32 [M][ldo]
+    float* trash;               // xgemm_pt: >= BN floats, the store target of rows past M
     int ldo;
     int act;
     // split K (EPI_BIAS, one kt-1 segment, no residual, bias or activation):
@@ -73,6 +74,11 @@ __host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain
 // epi: EPI_BIAS (cgemm.h: bias + residual + activation) or EPI_GRAPH (graph
 // mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
+// the persistent EPI_BIAS variant (xgemm_pt_kernel): <= 2 workgroups per CU
+// (ncu = compute units) walk the tiles with one DMA pipeline across tiles.
+// Needs Nc % bn == 0, >= 2 K steps, a.trash; identity residual read in the
+// epilogue (no identity K steps); bit-identical to launch_xgemm with epi_lds.
+hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st);
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
 // out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)

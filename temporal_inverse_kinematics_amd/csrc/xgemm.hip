@@ -649,6 +649,337 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     trace_out();
 }
 
+// ---------------------------------------------------------------------------
+// Persistent temporal-conv kernel (EPI_BIAS, 4 waves, two workgroups per CU):
+// each workgroup walks tiles b, b + G, b + 2G, ... and its DMA pipeline runs
+// ACROSS tiles — the next tile's first A and B stages are issued during the
+// current tile's last two K steps, and its step-0 A split runs under the
+// current tile's last MFMAs — so no tile pays a prologue (the first DMA round
+// trip) and the epilogue's stores drain under the next tile's K loop.
+// Epilogue (from the registers of the finished tile): global operands first
+// (bias, identity-residual rows, layer 0's residual-conv rows), then per
+// quarter of its 32 rows each wave stages 8 rows in the free B slot and
+// stores them row-major (whole 128-B lines). Rows past M store to a_trash, so
+// every wave issues the same count of vector-memory ops per tile and the
+// vmcnt waits stay exact. Same arithmetic, in the same order, as
+// xgemm_kernel with the LDS epilogue: bit-identical output.
+template <int BN>
+__global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
+    using C = XCfg<BN, EPI_BIAS, 4>;
+    constexpr int NW = 4, FM = C::FM, FN = C::FN, NIA = C::NIA, NIBW = C::NIBW, RW = C::RW, BM = C::BM;
+    static_assert(C::NIB_TOT % NW == 0 && C::LB == 1 && C::NSA == 2 && C::NSB == 2, "pt pipeline");
+    constexpr int LDC = BN + 4, LPR = BN / 4, RPI = 64 / LPR, NQ = 8 / RPI;   // staging: 8 rows per quarter
+    static_assert(8 * LDC * 4 * NW <= C::BBYTES, "staging fits one B slot");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4;
+    const int V = a.V;
+    const int ntn = a.Nc / BN;                          // column tiles
+    const int ntot = ((a.M + BM - 1) / BM) * ntn;       // tiles
+    const int G = gridDim.x, b = blockIdx.x;
+    const int my = b < ntot ? (ntot - 1 - b) / G + 1 : 0;
+    if (my == 0) return;
+    const int K = xgemm_kmain(a);                       // K steps per tile (all with weights)
+    const int total = my * K;
+    // tile i of this workgroup -> (first row, column tile): XCD-aware order over
+    // the linear id b + i G (G % 8 == 0: the XCD of the id is the workgroup's)
+    auto tile_of = [&](int i, int& r0, int& nt) __attribute__((always_inline)) {
+        const int L = b + i * G;
+        const int per = ntot >> 3, rem = ntot & 7, x = L & 7, k = L >> 3;
+        const int swz = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        r0 = (swz / ntn) * BM;
+        nt = swz - (swz / ntn) * ntn;
+    };
+
+    // ---- A cursor: tile ia, (segment, tap, block) within it, global step ga
+    int a_n[NIA], a_t[NIA], a_w[NIA], a_uo[NIA];
+    bool a_ok[NIA];
+#pragma unroll
+    for (int j = 0; j < NIA; ++j) {
+        const int rr = (wave * NIA + j) * 8 + (lane >> 3);
+        const int pl = (lane & 7) ^ xa_swz(rr);
+        a_uo[j] = 32 * (pl & 3) + 16 * (pl >> 2);
+    }
+    auto set_rows = [&](int r0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NIA; ++j) {
+            const int row = r0 + (wave * NIA + j) * 8 + (lane >> 3);
+            a_ok[j] = row < a.M;
+            const int q = a_ok[j] ? row / V : 0;
+            a_w[j] = a_ok[j] ? row - q * V : 0;
+            a_n[j] = q / a.tout;
+            a_t[j] = q - a_n[j] * a.tout;
+        }
+    };
+    const bool two = a.nseg > 1;
+    const unsigned nbk = (unsigned)((a.seg[0].cin >> 5) | (a.seg[0].kt << 8)) |
+                         ((unsigned)(two ? (a.seg[1].cin >> 5) | (a.seg[1].kt << 8) : 0) << 16);
+    int ia = 0, ca_seg = 0, ca_tap = 0, ca_blk = 0, ga = 0;
+    {
+        int r0, nt;
+        tile_of(0, r0, nt);
+        set_rows(r0);
+    }
+    unsigned a_off[NIA];
+    i32x4 rA;
+    bool a_stale = true;
+    auto prepare = [&]() __attribute__((always_inline)) {
+        if (!a_stale) return;
+        const XSeg sg = ca_seg == 0 ? a.seg[0] : a.seg[1];
+        rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
+#pragma unroll
+        for (int j = 0; j < NIA; ++j) {
+            const int t = sg.stride * a_t[j] + ca_tap - sg.pad;
+            a_off[j] = (a_ok[j] && t >= 0 && t < sg.tin)
+                           ? (unsigned)(((a_n[j] * sg.tin + t) * V + a_w[j]) * sg.ld * 4 + a_uo[j])
+                           : DMA_OOB;
+        }
+        a_stale = false;
+    };
+    auto a_slot = [&](int s) __attribute__((always_inline)) { return smem + s * C::ABYTES; };
+    auto b_slot = [&](int s) __attribute__((always_inline)) { return smem + 2 * C::ABYTES + s * C::BBYTES; };
+    auto issue_a = [&]() __attribute__((always_inline)) {
+        prepare();
+        unsigned char* A = a_slot(ga & 1);
+        const int soA = __builtin_amdgcn_readfirstlane(ca_blk * 128);
+#pragma unroll
+        for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
+        ++ga;
+        const unsigned f = nbk >> (16 * ca_seg);
+        const int seg = ca_seg, tap = ca_tap;
+        if (++ca_blk >= (int)(f & 255u)) {
+            ca_blk = 0;
+            if (++ca_tap >= (int)((f >> 8) & 255u)) {
+                ca_tap = 0;
+                if (++ca_seg >= a.nseg) {   // the tile's last K step: on to the next tile
+                    ca_seg = 0;
+                    if (++ia < my) {
+                        int r0, nt;
+                        tile_of(ia, r0, nt);
+                        set_rows(r0);
+                    }
+                }
+            }
+        }
+        a_stale = ca_seg != seg || ca_tap != tap || ca_blk == 0;
+    };
+    // ---- B cursor: tile ib (its column tile ntb), K step kbi, global step gb
+    int ib = 0, kbi = 0, gb = 0, ntb;
+    {
+        int r0;
+        tile_of(0, r0, ntb);
+    }
+    const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)ntn * K * C::BBYTES));
+    auto issue_b = [&]() __attribute__((always_inline)) {
+        unsigned char* Bd = b_slot(gb & 1);
+        const int soB = __builtin_amdgcn_readfirstlane((ntb * K + kbi) * C::BBYTES);
+#pragma unroll
+        for (int q = 0; q < NIBW; ++q)
+            dma16(rB, Bd + (wave + q * NW) * 1024, (unsigned)((wave + q * NW) * 1024 + lane * 16), soB);
+        ++gb;
+        if (++kbi == K) {
+            kbi = 0;
+            if (++ib < my) {
+                int r0;
+                tile_of(ib, r0, ntb);
+            }
+        }
+    };
+
+    // ---- epilogue operands that do not change per tile
+    const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
+    const int cl = 4 * (lane % LPR), rsub = lane / LPR;
+    const bool has_b = a.bias != nullptr, has_i = a.idn.src != nullptr, has_x = BN == 64 && a.rx != nullptr;
+    float rw[4][4];   // layer 0's residual conv (one column tile: the launch checks)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) rw[e][c] = has_x && c < a.rxc ? a.rw[(cl + e) * a.rxc + c] : 0.f;
+    // vector-memory ops one epilogue issues per wave (all unconditional)
+    const int E = (has_b ? 1 : 0) + 4 * NQ * ((has_i ? 1 : 0) + (has_x ? 1 : 0) + 1);
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int bsw = (-((lane & 15) >> 2)) & 3;
+    const int boff = (lane & 15) * 64 + ((g ^ bsw) << 4);
+    auto mma = [&](const xbf16x8& x, const xbf16x8& w, f32x4& c) __attribute__((always_inline)) {
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);   // transposed: lane = row (l & 15), 4 channels
+    };
+    auto read_a = [&](int s, f32x4 (&lo)[FM], f32x4 (&hi)[FM]) __attribute__((always_inline)) {
+        const unsigned char* A = a_slot(s & 1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int r = wave * RW + i * 16 + (lane & 15);
+            lo[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + ((g ^ xa_swz(r)) << 4));
+            hi[i] = *reinterpret_cast<const f32x4*>(A + r * 128 + (((g + 4) ^ xa_swz(r)) << 4));
+        }
+    };
+
+    // epilogue of the finished tile ic (its last K step used B slot `slot`)
+    auto epilogue = [&](int ic, int slot) __attribute__((always_inline)) {
+        int r0, nt;
+        tile_of(ic, r0, nt);
+        const int col = nt * BN + cl;
+        // global operands first (a load issued after a store would wait for it)
+        const f32x4 bv = has_b ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 xi[4][NQ], xr[4][NQ];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rr = 0; rr < NQ; ++rr) {
+                const int row = r0 + wave * RW + 16 * (q >> 1) + 8 * (q & 1) + rr * RPI + rsub;
+                const int rc = row < a.M ? row : 0;   // rows past M read row 0 (discarded)
+                xi[q][rr] = has_i ? *reinterpret_cast<const f32x4*>(a.idn.src + (size_t)rc * a.idn.ld + col)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+                xr[q][rr] = has_x ? *reinterpret_cast<const f32x4*>(a.rx + (size_t)rc * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        float* st = reinterpret_cast<float*>(b_slot(slot)) + wave * 8 * LDC;
+        __syncthreads();   // every wave done reading B slot `slot` (the last K step's weights)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = q >> 1, h = q & 1;
+            if (((lane & 15) >> 3) == h)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(st + (lane & 7) * LDC + 16 * j + 4 * g) = acc[i][j];
+#pragma unroll
+            for (int rr = 0; rr < NQ; ++rr) {
+                const int lr = rr * RPI + rsub;
+                const int row = r0 + wave * RW + 16 * i + 8 * h + lr;
+                f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * LDC + cl);
+                if (has_i) v += xi[q][rr];   // (acc + x) + bias, as xgemm_kernel
+                v += bv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (has_x) v[e] += xr[q][rr][0] * rw[e][0] + xr[q][rr][1] * rw[e][1] + xr[q][rr][2] * rw[e][2] + xr[q][rr][3] * rw[e][3];
+                    v[e] = v[e] > 0.f ? v[e] : slope * v[e];
+                }
+                float* dst = row < a.M ? a.out + (size_t)row * a.ldo + col : a.trash + cl;
+                *reinterpret_cast<f32x4*>(dst) = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+
+    xbf16x8 c0[FM], c1[FM], c2[FM], d0[FM], d1[FM], d2[FM];
+    f32x4 alo[FM], ahi[FM];
+    // prologue (the first tile only): B(0) A(0) A(1)
+    issue_b();
+    issue_a();
+    if (total > 1) issue_a();
+    if (total > 1) wait_vm<NIA>();
+    else wait_vm<0>();
+    read_a(0, alo, ahi);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) xsplit8(alo[i], ahi[i], c0[i], c1[i], c2[i]);
+
+    int k = 0, ic = 0;   // the computing tile and its K step
+    // global step s: MFMAs of (tile ic, step k) on the split in u, with step
+    // s+1's A read and split into v (which may be the next tile's step 0)
+    auto step = [&](int s, auto steady, xbf16x8 (&u0)[FM], xbf16x8 (&u1)[FM], xbf16x8 (&u2)[FM], xbf16x8 (&v0)[FM],
+                    xbf16x8 (&v1)[FM], xbf16x8 (&v2)[FM]) __attribute__((always_inline)) {
+        constexpr bool ST = decltype(steady)::value;   // s + 2 < total: B(s+1) and A(s+2) exist
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // every wave's B(s) landed; every wave done with B(s-1) / the staging
+        if (ST || s + 1 < total) issue_b();
+        if (ST || s + 2 < total) issue_a();
+        // A(s+1) landed: younger are B(s+1), A(s+2), and after a tile boundary
+        // the E epilogue ops issued between A(s+1) and this step
+        if (ST) {
+            if (k == 0 && s > 0) wait_vm_dyn(NIA + NIBW + E);
+            else wait_vm<NIA + NIBW>();
+        } else {
+            wait_vm<0>();
+        }
+        const unsigned char* Bp = b_slot(s & 1) + boff;
+        xbf16x8 bb[2][3];
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(s + 1, alo, ahi);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bb[0][p] = *reinterpret_cast<const xbf16x8*>(Bp + p * C::PLANE);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            if (j + 1 < FN)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bb[(j + 1) & 1][p] = *reinterpret_cast<const xbf16x8*>(Bp + p * C::PLANE + (j + 1) * 16 * 64);
+            const xbf16x8(&bq)[3] = bb[j & 1];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                mma(u2[i], bq[0], acc[i][j]);
+                mma(u1[i], bq[1], acc[i][j]);
+                mma(u0[i], bq[2], acc[i][j]);
+                mma(u1[i], bq[0], acc[i][j]);
+                mma(u0[i], bq[1], acc[i][j]);
+                mma(u0[i], bq[0], acc[i][j]);
+            }
+            if (j < FM) xsplit8(alo[j], ahi[j], v0[j], v1[j], v2[j]);
+            if (j == FN - 1)
+#pragma unroll
+                for (int i = FN; i < FM; ++i) xsplit8(alo[i], ahi[i], v0[i], v1[i], v2[i]);
+            if (j + 1 < FN) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int q = 0; q < 6 * FM; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // B(s+1) landed before the next barrier (only A(s+2) younger)
+        if (ST) wait_vm<NIA>();
+        else wait_vm<0>();
+        if (++k == K) {
+            epilogue(ic, s & 1);
+            k = 0;
+            ++ic;
+        }
+    };
+    const std::true_type steady{};
+    const std::false_type general{};
+    int s = 0;
+    for (; s + 3 < total; s += 2) {
+        step(s, steady, c0, c1, c2, d0, d1, d2);
+        step(s + 1, steady, d0, d1, d2, c0, c1, c2);
+    }
+    for (; s < total; s += 2) {
+        step(s, general, c0, c1, c2, d0, d1, d2);
+        if (s + 1 < total) step(s + 1, general, d0, d1, d2, c0, c1, c2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st) {
+    if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
+    const int kall = xgemm_kmain(a);
+    if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || a.ldo % 4 || a.Nc % bn || a.nseg < 1 || a.nseg > 2 ||
+        kall < 2 || a.ksplit > 1 || (a.nw != 0 && a.nw != 4))
+        return hipErrorInvalidValue;
+    for (int s = 0; s <= a.nseg; ++s) {
+        const XSeg& g = s < a.nseg ? a.seg[s] : a.idn;
+        if (s == a.nseg && !g.src) break;
+        if (!g.src || g.cin % 32 || g.ld % 4 || g.ld < g.cin || g.rows_in * g.ld * 4 >= (1LL << 31)) return hipErrorInvalidValue;
+    }
+    if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
+        return hipErrorInvalidValue;
+    if (a.rx && (bn != 64 || a.Nc != bn || a.rxc < 0 || a.rxc > 4 || !a.rw)) return hipErrorInvalidValue;
+    if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
+    const long long ntot = (long long)((a.M + 127) / 128) * (a.Nc / bn);
+    long long G = std::min<long long>(ntot, 2LL * ncu);
+    if (G > 8) G &= ~7LL;   // a multiple of 8: tile id b + i G stays on the workgroup's XCD
+    (void)hipGetLastError();
+    if (bn == 128) hipLaunchKernelGGL(xgemm_pt_kernel<128>, dim3((unsigned)G), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(xgemm_pt_kernel<64>, dim3((unsigned)G), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 int xgemm_tile_rows(int epi, int nw) {
     const int bm = 32 * (nw == 8 ? 8 : 4);
     return epi == EPI_GRAPH ? bm / 17 * 17 : bm;

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
+@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xpt", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
                                                  "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
                                                  "f16x3-dmahead"])
 def model(request):
@@ -46,7 +46,9 @@ def model(request):
                "xnw8": {"TIK_XNW": "8"},
                # xgemm temporal-conv epilogue from registers (half-line stores), and through LDS
                # with the identity residual as extra K steps (default: loaded in the epilogue)
-               "xepi0": {"TIK_XEPI": "0"}, "xepi1": {"TIK_XEPI": "1"}}.get(path, {"TIK_GEMM_PATH": path})
+               "xepi0": {"TIK_XEPI": "0"}, "xepi1": {"TIK_XEPI": "1"},
+               # temporal convs on the persistent kernel (DMA pipeline across tiles)
+               "xpt": {"TIK_XPT": "255"}}.get(path, {"TIK_GEMM_PATH": path})
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created
@@ -486,3 +488,20 @@ def test_bf16x3_batch_invariant_bitwise():
         assert torch.equal(part, full[:37])
         for i in (0, 36, 511, 1023):
             assert torch.equal(m(x[i:i + 1])["poses"], full[i:i + 1]), i
+
+
+@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65)])
+def test_xgemm_persistent_bitwise(n, T):
+    """The persistent temporal-conv kernel (TIK_XPT=255: one DMA pipeline across
+    each workgroup's tiles, epilogue operands loaded up front, rows past M
+    stored to a trash line) computes every row with the same operations in the
+    same order as the per-tile kernel: bit-identical poses, including batches
+    whose last tile is partial and batches with fewer tiles than workgroups."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    pt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=255)
+    one = _model_with_env("bf16x3", TIK_SPLIT=0)
+    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + T)).cuda()
+    with torch.no_grad():
+        a = pt(x)["poses"].clone()
+        b = one(x)["poses"]
+    assert torch.equal(a, b), float((a - b).abs().max())

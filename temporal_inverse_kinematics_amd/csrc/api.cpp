@@ -234,7 +234,7 @@ struct Layer {
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
-    int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; TIK_XPT bit mask of layers)
+    int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
@@ -917,7 +917,9 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
             for (auto& L : md->layers) L.ncu = ncu;
         const char* e = getenv("TIK_XPT");
         for (auto& L : md->layers) {
-            L.xpt = e ? (atoi(e) >> L.index) & 1 : 0;   // TIK_XPT: bit l = layer l (255: all)
+            // default: the 64-column temporal convs (6 K steps per tile: the
+            // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
+            L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
             L.xtrash = reinterpret_cast<float*>(md->trash.p);
         }
     }

@@ -669,7 +669,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     constexpr int NW = 4, FM = C::FM, FN = C::FN, NIA = C::NIA, NIBW = C::NIBW, RW = C::RW, BM = C::BM;
     static_assert(C::NIB_TOT % NW == 0 && C::LB == 1 && C::NSA == 2 && C::NSB == 2, "pt pipeline");
     constexpr int LDC = BN + 4, LPR = BN / 4, RPI = 64 / LPR, NQ = 8 / RPI;   // staging: 8 rows per quarter
-    static_assert(8 * LDC * 4 * NW <= C::BBYTES, "staging fits one B slot");
+    static_assert(9 * LDC * 4 * NW <= C::BBYTES, "staging (8 rows + a dummy row per wave) fits one B slot");
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -838,14 +838,19 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                                   : f32x4{0.f, 0.f, 0.f, 0.f};
                 xr[q][rr] = has_x ? *reinterpret_cast<const f32x4*>(a.rx + (size_t)rc * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
-        float* st = reinterpret_cast<float*>(b_slot(slot)) + wave * 8 * LDC;
-        __syncthreads();   // every wave done reading B slot `slot` (the last K step's weights)
+        float* st = reinterpret_cast<float*>(b_slot(slot)) + wave * 9 * LDC;
+        // every wave done reading B slot `slot` (the last K step's weights); no
+        // __syncthreads: its release fence would wait for every DMA in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int i = q >> 1, h = q & 1;
-            if (((lane & 15) >> 3) == h)
+            // every lane writes (the other half's lanes to a dummy 9th row): with a
+            // divergent `if` here hipcc sank the following read into the masked block
+            const int wr = ((lane & 15) >> 3) == h ? (lane & 7) : 8;
 #pragma unroll
-                for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(st + (lane & 7) * LDC + 16 * j + 4 * g) = acc[i][j];
+            for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(st + wr * LDC + 16 * j + 4 * g) = acc[i][j];
 #pragma unroll
             for (int rr = 0; rr < NQ; ++rr) {
                 const int lr = rr * RPI + rsub;

@@ -430,7 +430,7 @@ struct Layer {
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
         t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger();
-        const bool pt = xpt && xtrash && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
+        const bool pt = xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
         const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);

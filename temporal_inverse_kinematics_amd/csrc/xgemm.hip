@@ -663,7 +663,8 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
 // every wave issues the same count of vector-memory ops per tile and the
 // vmcnt waits stay exact. Same arithmetic, in the same order, as
 // xgemm_kernel with the LDS epilogue: bit-identical output.
-template <int BN>
+// IDN: identity residual (block input rows); RX: layer 0's residual conv rows
+template <int BN, bool IDN, bool RX>
 __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     using C = XCfg<BN, EPI_BIAS, 4>;
     constexpr int NW = 4, FM = C::FM, FN = C::FN, NIA = C::NIA, NIBW = C::NIBW, RW = C::RW, BM = C::BM;
@@ -791,14 +792,35 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     // ---- epilogue operands that do not change per tile
     const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
     const int cl = 4 * (lane % LPR), rsub = lane / LPR;
-    const bool has_b = a.bias != nullptr, has_i = a.idn.src != nullptr, has_x = BN == 64 && a.rx != nullptr;
+    constexpr bool has_i = IDN, has_x = BN == 64 && RX;   // the bias is always there (the launch checks)
     float rw[4][4];   // layer 0's residual conv (one column tile: the launch checks)
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < 4; ++c) rw[e][c] = has_x && c < a.rxc ? a.rw[(cl + e) * a.rxc + c] : 0.f;
-    // vector-memory ops one epilogue issues per wave (all unconditional)
-    const int E = (has_b ? 1 : 0) + 4 * NQ * ((has_i ? 1 : 0) + (has_x ? 1 : 0) + 1);
+    // vector-memory ops per wave (all unconditional): the epilogue operand loads,
+    // issued at the start of a tile's last K step (before its DMAs), and the
+    // epilogue's stores
+    constexpr int NXL = 1 + 4 * NQ * ((has_i ? 1 : 0) + (has_x ? 1 : 0)), NST = 4 * NQ;
+    // early (during the last K step): 64 more live VGPRs there; the 128-column
+    // identity variant would spill, so it loads at the epilogue start instead
+    constexpr bool EARLY = !(BN == 128 && IDN);
+    f32x4 bv, xi[4][NQ], xr[4][NQ];
+    auto load_epi = [&](int ic) __attribute__((always_inline)) {
+        int r0, nt;
+        tile_of(ic, r0, nt);
+        const int col = nt * BN + cl;
+        bv = *reinterpret_cast<const f32x4*>(a.bias + col);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rr = 0; rr < NQ; ++rr) {
+                const int row = r0 + wave * RW + 16 * (q >> 1) + 8 * (q & 1) + rr * RPI + rsub;
+                const int rc = row < a.M ? row : 0;   // rows past M read row 0 (discarded)
+                if constexpr (has_i) xi[q][rr] = *reinterpret_cast<const f32x4*>(a.idn.src + (size_t)rc * a.idn.ld + col);
+                if constexpr (has_x) xr[q][rr] = *reinterpret_cast<const f32x4*>(a.rx + (size_t)rc * 4);
+            }
+    };
 
     f32x4 acc[FM][FN];
 #pragma unroll
@@ -825,19 +847,8 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         int r0, nt;
         tile_of(ic, r0, nt);
         const int col = nt * BN + cl;
-        // global operands first (a load issued after a store would wait for it)
-        const f32x4 bv = has_b ? *reinterpret_cast<const f32x4*>(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 xi[4][NQ], xr[4][NQ];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int rr = 0; rr < NQ; ++rr) {
-                const int row = r0 + wave * RW + 16 * (q >> 1) + 8 * (q & 1) + rr * RPI + rsub;
-                const int rc = row < a.M ? row : 0;   // rows past M read row 0 (discarded)
-                xi[q][rr] = has_i ? *reinterpret_cast<const f32x4*>(a.idn.src + (size_t)rc * a.idn.ld + col)
-                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-                xr[q][rr] = has_x ? *reinterpret_cast<const f32x4*>(a.rx + (size_t)rc * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+        // bv, xi, xr: loaded by load_epi at the start of the tile's last K step (EARLY) or now
+        if constexpr (!EARLY) load_epi(ic);
         float* st = reinterpret_cast<float*>(b_slot(slot)) + wave * 9 * LDC;
         // every wave done reading B slot `slot` (the last K step's weights); no
         // __syncthreads: its release fence would wait for every DMA in flight
@@ -856,11 +867,11 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                 const int lr = rr * RPI + rsub;
                 const int row = r0 + wave * RW + 16 * i + 8 * h + lr;
                 f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * LDC + cl);
-                if (has_i) v += xi[q][rr];   // (acc + x) + bias, as xgemm_kernel
+                if constexpr (has_i) v += xi[q][rr];   // (acc + x) + bias, as xgemm_kernel
                 v += bv;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (has_x) v[e] += xr[q][rr][0] * rw[e][0] + xr[q][rr][1] * rw[e][1] + xr[q][rr][2] * rw[e][2] + xr[q][rr][3] * rw[e][3];
+                    if constexpr (has_x) v[e] += xr[q][rr][0] * rw[e][0] + xr[q][rr][1] * rw[e][1] + xr[q][rr][2] * rw[e][2] + xr[q][rr][3] * rw[e][3];
                     v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                 }
                 float* dst = row < a.M ? a.out + (size_t)row * a.ldo + col : a.trash + cl;
@@ -893,12 +904,16 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         constexpr bool ST = decltype(steady)::value;   // s + 2 < total: B(s+1) and A(s+2) exist
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();   // every wave's B(s) landed; every wave done with B(s-1) / the staging
+        const bool last = k == K - 1;
+        if (EARLY && last) load_epi(ic);   // the epilogue's global operands, a whole K step ahead
         if (ST || s + 1 < total) issue_b();
         if (ST || s + 2 < total) issue_a();
-        // A(s+1) landed: younger are B(s+1), A(s+2), and after a tile boundary
-        // the E epilogue ops issued between A(s+1) and this step
+        // A(s+1) landed: younger are B(s+1), A(s+2), plus the epilogue loads just
+        // issued (a tile's last step) or the stores of the epilogue that ended the
+        // previous tile (its first step)
         if (ST) {
-            if (k == 0 && s > 0) wait_vm_dyn(NIA + NIBW + E);
+            if (EARLY && last) wait_vm<NIA + NIBW + NXL>();
+            else if (k == 0 && s > 0) wait_vm<NIA + NIBW + NST + (EARLY ? 0 : NXL)>();
             else wait_vm<NIA + NIBW>();
         } else {
             wait_vm<0>();
@@ -964,7 +979,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
 hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     const int kall = xgemm_kmain(a);
-    if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || a.ldo % 4 || a.Nc % bn || a.nseg < 1 || a.nseg > 2 ||
+    if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || !a.bias || a.ldo % 4 || a.Nc % bn || a.nseg < 1 || a.nseg > 2 ||
         kall < 2 || a.ksplit > 1 || (a.nw != 0 && a.nw != 4))
         return hipErrorInvalidValue;
     for (int s = 0; s <= a.nseg; ++s) {
@@ -974,14 +989,21 @@ hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st) {
     }
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
-    if (a.rx && (bn != 64 || a.Nc != bn || a.rxc < 0 || a.rxc > 4 || !a.rw)) return hipErrorInvalidValue;
+    if (a.rx && (bn != 64 || a.Nc != bn || a.rxc < 0 || a.rxc > 4 || !a.rw || a.idn.src)) return hipErrorInvalidValue;
     if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const long long ntot = (long long)((a.M + 127) / 128) * (a.Nc / bn);
     long long G = std::min<long long>(ntot, 2LL * ncu);
     if (G > 8) G &= ~7LL;   // a multiple of 8: tile id b + i G stays on the workgroup's XCD
     (void)hipGetLastError();
-    if (bn == 128) hipLaunchKernelGGL(xgemm_pt_kernel<128>, dim3((unsigned)G), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(xgemm_pt_kernel<64>, dim3((unsigned)G), dim3(256), 0, st, a);
+    const dim3 grid((unsigned)G), blk(256);
+    if (bn == 128) {
+        if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<128, true, false>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((xgemm_pt_kernel<128, false, false>), grid, blk, 0, st, a);
+    } else {
+        if (a.rx) hipLaunchKernelGGL((xgemm_pt_kernel<64, false, true>), grid, blk, 0, st, a);
+        else if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<64, true, false>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((xgemm_pt_kernel<64, false, false>), grid, blk, 0, st, a);
+    }
     return hipGetLastError();
 }
 

@@ -68,7 +68,8 @@ def kernel_symbol(label, precision):
         nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
         return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
     if label[:2] == "XP" and label[2:] in ("64", "128"):
-        return f"tik::xgemm_pt_kernel<{label[2:]}>"
+        # xgemm_pt_kernel<BN, identity, residual conv>: the label does not say which (any instantiation)
+        return "tik::xgemm_pt_kernel"
     if label == "XR":
         return "tik::xgemm_splitk_reduce_kernel"
     p = PREC_CODE[precision]

@@ -7,8 +7,8 @@
 //   tgemm (TG_128x128)  v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
 //   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// (f16x3 on split-block operands; bf16x3: the blend shapes on xgemm.hip and
-// the skinning on cgemm.hip; fp32 both on cgemm.hip)
+// (f16x3 on split-block operands; bf16x3: both on xgemm.hip, the skinning
+// with its own epilogue EPI_SKIN; fp32 both on cgemm.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,6 +39,7 @@ struct tik_fk {
     SplitW3 s3PT, s3WT;   // bf16 planes p0+p1+p2 (bf16x3 register-staged GEMMs)
     SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
+    DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the skinning GEMM, EPI_SKIN)
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
     DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra, depth;
@@ -180,8 +181,8 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
     }
     const char* xe = getenv("TIK_FK_XGEMM");
     if (!(xe && xe[0] == '0')) {
-        const tik::XPackSeg ps{PT.data(), KP, 1, KP};
-        if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128)))) {
+        const tik::XPackSeg ps{PT.data(), KP, 1, KP}, ws{WT.data(), KJ, 1, KJ};
+        if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128))) || (rc = fk->xWT.upload(tik::xgemm_pack(&ws, 1, V, 128)))) {
             delete fk;
             return rc;
         }
@@ -284,6 +285,15 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
         }
 
+        if (fk->prec == tik::PREC_BF16X3 && fk->xWT.p) {
+            // skinning + vertex transform on xgemm.hip (EPI_SKIN)
+            tik::XArgs s{};
+            s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
+            s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * 16, (long long)B * 16};
+            s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s);
+            s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl; s.act = tik::ACT_NONE;
+            HIP_TRY(tik::launch_xgemm(s, 128, tik::EPI_SKIN, st));
+        } else {
         tik::CgemmArgs s{};   // skinning + vertex transform
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
         s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
@@ -291,6 +301,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         for (int i = 0; i < 3; ++i) s.seg[0].wb[i] = fk->s3WT.p[i].p;
         s.nseg = 1; s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl;
         HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
+        }
     }
 
     tik::FkLmkArgs l{};

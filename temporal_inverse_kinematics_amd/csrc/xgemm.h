@@ -47,6 +47,8 @@ struct XArgs {
     const float* rw;            // its weights [Nc][rxc]
     const float* amix;          // EPI_GRAPH [V][V], A_eff[v][w]
     int mix_sparse;
+    const float* resid;         // EPI_SKIN: v_posed [M/16][ldr] (bodies x 3V), out = verts [M/16][ldo], bias = transl [M/16][3] or null
+    int ldr;
     float* out;                 // fp32 [M][ldo]
     float* trash;               // xgemm_pt: >= BN floats, the store target of rows past M
     int ldo;
@@ -71,8 +73,9 @@ __host__ __device__ inline int xgemm_kmain(const XArgs& a) {
 }
 __host__ __device__ inline int xgemm_ksteps(const XArgs& a) { return xgemm_kmain(a) + (a.idn.src ? a.idn.cin / 32 : 0); }
 
-// epi: EPI_BIAS (cgemm.h: bias + residual + activation) or EPI_GRAPH (graph
-// mix over the 17 joints + bias2[w][c] + ReLU); bn: 64 or 128 output columns per tile
+// epi: EPI_BIAS (cgemm.h: bias + residual + activation), EPI_GRAPH (graph
+// mix over the 17 joints + bias2[w][c] + ReLU) or EPI_SKIN (SMPL-X skinning:
+// rows = body * 16 + transform entry, columns = vertices); bn: 64 or 128 output columns per tile
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 // the persistent EPI_BIAS variant (xgemm_pt_kernel): <= 2 workgroups per CU
 // (ncu = compute units) walk the tiles with one DMA pipeline across tiles.

@@ -121,7 +121,7 @@ struct XCfg {
     static constexpr int RT = EPI == EPI_GRAPH ? BM / 17 * 17 : BM;   // valid rows per tile (whole frames for the mix)
     static constexpr int LDCG = BN + 4;
     // C tile (+ the bias2 slice for the graph mix)
-    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : BM * LDCG * 4;
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : (EPI == EPI_SKIN ? 0 : BM * LDCG * 4);
     static constexpr int SMEM = RING > CT ? RING : CT;
     static constexpr int WG_PER_CU = NW == 8 ? 1 : 2;
     static_assert(NIA * 1024 * NW == ABYTES && NIA * 8 == RW, "A DMA split");
@@ -599,6 +599,40 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 }
             }
         }
+    } else if constexpr (EPI == EPI_SKIN) {
+        // ---- SMPL-X skinning (lbs): rows = body * 16 + transform entry e of
+        // T_v(b) = sum_j W[v][j] A_j(b); a 16-row fragment is one body and lane
+        // group g holds entries 4g..4g+3 = transform row g of vertex n0 + 16j +
+        // (lane & 15). verts[b][3v + g] = T[g][:3] . v_posed[b][3v..] + T[g][3]
+        // (+ transl[b][g]), the fma chain of cgemm.hip's EPI_SKIN.
+        // Every global operand is loaded before the first store.
+        const int vl = lane & 15;
+        float vpr[FM][FN][3], tb[FM];
+        int bdy[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            bdy[i] = (r0 + wave * RW + 16 * i) >> 4;
+            const bool bok = g < 3 && bdy[i] * 16 < a.M;
+            tb[i] = bok && a.bias ? a.bias[bdy[i] * 3 + g] : 0.f;
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int v = n0 + 16 * j + vl;
+                const float* vp = a.resid + (size_t)bdy[i] * a.ldr + 3 * v;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) vpr[i][j][c] = bok && v < a.Nc ? vp[c] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int v = n0 + 16 * j + vl;
+                if (g < 3 && bdy[i] * 16 < a.M && v < a.Nc) {
+                    const f32x4 t = acc[i][j];
+                    const float x = fmaf(t[0], vpr[i][j][0], fmaf(t[1], vpr[i][j][1], fmaf(t[2], vpr[i][j][2], t[3])));
+                    a.out[(size_t)bdy[i] * a.ldo + 3 * v + g] = x + tb[i];
+                }
+            }
     } else {
         // ---- EPI_GRAPH: the C tile through LDS, then the graph mix per frame
         float* Cs = reinterpret_cast<float*>(smem);
@@ -1014,7 +1048,8 @@ int xgemm_tile_rows(int epi, int nw) {
 
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
-    if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH) || !a.wp || !a.out || a.ldo % 4 ||
+    if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH && epi != EPI_SKIN) || !a.wp || !a.out ||
+        (epi != EPI_SKIN && a.ldo % 4) ||
         a.nseg < 1 || a.nseg > 2 || a.ksteps != xgemm_ksteps(a) || xgemm_kmain(a) <= 0)
         return hipErrorInvalidValue;
     for (int s = 0; s <= a.nseg; ++s) {
@@ -1026,7 +1061,9 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.rx && (bn != 64 || epi != EPI_BIAS || a.rxc < 0 || a.rxc > 4)) return hipErrorInvalidValue;
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
-    if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
+    if (epi == EPI_SKIN && (a.M % 16 || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx || a.nw == 8))
+        return hipErrorInvalidValue;
+    if ((long long)(epi == EPI_SKIN ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const int nw = a.nw == 8 ? 8 : 4, rt = xgemm_tile_rows(epi, nw);
     if (a.nw != 0 && a.nw != 4 && a.nw != 8) return hipErrorInvalidValue;
     const int ks = a.ksplit > 1 ? a.ksplit : 1;
@@ -1043,6 +1080,9 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
         if (bn == 128 && nw == 4) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 4, true>), grid, blk, 0, st, a);
         else if (bn == 128) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 8, true>), grid, blk, 0, st, a);
         else return hipErrorInvalidValue;
+    } else if (epi == EPI_SKIN) {
+        if (bn == 128) XL(128, EPI_SKIN, 4);
+        else XL(64, EPI_SKIN, 4);
     } else if (nw == 4) {
         if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 4); else XL(128, EPI_GRAPH, 4); }
         else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 4); else XL(64, EPI_GRAPH, 4); }

@@ -140,6 +140,6 @@ def test_bench_kernel_symbols_match_pmc_profile():
     assert max(tags, key=lambda s: (int(s[1:3]), int(s.split("_v")[1].rstrip("_")))) in os.path.basename(newest)
     kernels = json.load(open(newest))["kernels"]
     # the default (bf16x3) path's launches
-    for label in ("XT128", "XG128", "XT64", "XG64", "XH128", "XR"):
+    for label in ("XT128", "XG128", "XP64", "XG64", "XH128", "XR"):
         traffic, src = bench._pmc_traffic(newest, label, "bf16x3")
         assert traffic is not None and traffic > 0, (label, bench.kernel_symbol(label, "bf16x3"), list(kernels))

@@ -40,6 +40,8 @@ struct tik_fk {
     SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
     DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the skinning GEMM, EPI_SKIN)
+    bool xpt = true;   // skinning on the persistent xgemm kernel (TIK_FK_PT=0: one workgroup per tile)
+    int ncu = 256;
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
     DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra, depth;
@@ -179,6 +181,12 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         delete fk;
         return rc;
     }
+    if (const char* e = getenv("TIK_FK_PT")) fk->xpt = e[0] != '0';
+    {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            fk->ncu = n;
+    }
     const char* xe = getenv("TIK_FK_XGEMM");
     if (!(xe && xe[0] == '0')) {
         const tik::XPackSeg ps{PT.data(), KP, 1, KP}, ws{WT.data(), KJ, 1, KJ};
@@ -292,7 +300,13 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * 16, (long long)B * 16};
             s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s);
             s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl; s.act = tik::ACT_NONE;
-            HIP_TRY(tik::launch_xgemm(s, 128, tik::EPI_SKIN, st));
+            if (fk->xpt) {   // persistent: the DMA pipeline runs across tiles (K = 64 is 2 steps per tile)
+                s.bias = transl ? transl : fk->zero_transl.p;
+                s.trash = reinterpret_cast<float*>(fk->trash.p);
+                HIP_TRY(tik::launch_xgemm_pt(s, 128, fk->ncu, st, tik::EPI_SKIN));
+            } else {
+                HIP_TRY(tik::launch_xgemm(s, 128, tik::EPI_SKIN, st));
+            }
         } else {
         tik::CgemmArgs s{};   // skinning + vertex transform
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;

@@ -81,7 +81,8 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 // (ncu = compute units) walk the tiles with one DMA pipeline across tiles.
 // Needs Nc % bn == 0, >= 2 K steps, a.trash; identity residual read in the
 // epilogue (no identity K steps); bit-identical to launch_xgemm with epi_lds.
-hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st);
+// epi: EPI_BIAS or EPI_SKIN (bn 128, bias = translations (B,3), zeros if none).
+hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int epi = EPI_BIAS);
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
 // out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)

@@ -697,10 +697,13 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
 // every wave issues the same count of vector-memory ops per tile and the
 // vmcnt waits stay exact. Same arithmetic, in the same order, as
 // xgemm_kernel with the LDS epilogue: bit-identical output.
+// EPI: EPI_BIAS (temporal convs) or EPI_SKIN (SMPL-X skinning, the epilogue
+// of xgemm_kernel's EPI_SKIN from registers, non-transposed MFMA);
 // IDN: identity residual (block input rows); RX: layer 0's residual conv rows
-template <int BN, bool IDN, bool RX>
+template <int BN, int EPI, bool IDN, bool RX>
 __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
-    using C = XCfg<BN, EPI_BIAS, 4>;
+    constexpr bool SKIN = EPI == EPI_SKIN;
+    using C = XCfg<BN, EPI_BIAS, 4>;   // the same ring (EPI_SKIN needs no C tile)
     constexpr int NW = 4, FM = C::FM, FN = C::FN, NIA = C::NIA, NIBW = C::NIBW, RW = C::RW, BM = C::BM;
     static_assert(C::NIB_TOT % NW == 0 && C::LB == 1 && C::NSA == 2 && C::NSB == 2, "pt pipeline");
     constexpr int LDC = BN + 4, LPR = BN / 4, RPI = 64 / LPR, NQ = 8 / RPI;   // staging: 8 rows per quarter
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4;
     const int V = a.V;
-    const int ntn = a.Nc / BN;                          // column tiles
+    const int ntn = (a.Nc + BN - 1) / BN;               // column tiles (EPI_BIAS: Nc % BN == 0)
     const int ntot = ((a.M + BM - 1) / BM) * ntn;       // tiles
     const int G = gridDim.x, b = blockIdx.x;
     const int my = b < ntot ? (ntot - 1 - b) / G + 1 : 0;
@@ -835,14 +838,35 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     // vector-memory ops per wave (all unconditional): the epilogue operand loads,
     // issued at the start of a tile's last K step (before its DMAs), and the
     // epilogue's stores
-    constexpr int NXL = 1 + 4 * NQ * ((has_i ? 1 : 0) + (has_x ? 1 : 0)), NST = 4 * NQ;
+    // (EPI_SKIN: per lane FM x FN v_posed triples + FM translations; FM x FN scalar stores)
+    constexpr int NXL = SKIN ? FM * FN + FM : 1 + 4 * NQ * ((has_i ? 1 : 0) + (has_x ? 1 : 0));
+    constexpr int NST = SKIN ? FM * FN : 4 * NQ;
     // early (during the last K step): 64 more live VGPRs there; the 128-column
     // identity variant would spill, so it loads at the epilogue start instead
     constexpr bool EARLY = !(BN == 128 && IDN);
     f32x4 bv, xi[4][NQ], xr[4][NQ];
+    float vpr[SKIN ? FM : 1][SKIN ? FN : 1][3], tb[SKIN ? FM : 1];
     auto load_epi = [&](int ic) __attribute__((always_inline)) {
         int r0, nt;
         tile_of(ic, r0, nt);
+        if constexpr (SKIN) {
+            // row block of fragment i = body (r0 + 32 wave + 16 i) / 16; lane = vertex
+            // n0 + 16 j + (lane & 15), transform row g (g == 3 and rows / vertices past
+            // the end load valid dummies and store to a_trash)
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int b = (r0 + wave * RW + 16 * i) >> 4;
+                const int bb = b * 16 < a.M ? b : 0;
+                tb[i] = a.bias[bb * 3 + (g < 3 ? g : 0)];
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int v = nt * BN + 16 * j + (lane & 15);
+                    const float* vp = a.resid + (size_t)bb * a.ldr + 3 * (v < a.Nc ? v : 0);
+                    __builtin_memcpy(&vpr[i][j][0], vp, 12);   // one 12-B load
+                }
+            }
+            return;
+        }
         const int col = nt * BN + cl;
         bv = *reinterpret_cast<const f32x4*>(a.bias + col);
 #pragma unroll
@@ -864,7 +888,9 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     const int bsw = (-((lane & 15) >> 2)) & 3;
     const int boff = (lane & 15) * 64 + ((g ^ bsw) << 4);
     auto mma = [&](const xbf16x8& x, const xbf16x8& w, f32x4& c) __attribute__((always_inline)) {
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);   // transposed: lane = row (l & 15), 4 channels
+        // EPI_BIAS transposed (lane = row (l & 15), 4 channels); EPI_SKIN not (lane = vertex, 4 entries)
+        c = SKIN ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, w, c, 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);
     };
     auto read_a = [&](int s, f32x4 (&lo)[FM], f32x4 (&hi)[FM]) __attribute__((always_inline)) {
         const unsigned char* A = a_slot(s & 1);
@@ -880,6 +906,22 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     auto epilogue = [&](int ic, int slot) __attribute__((always_inline)) {
         int r0, nt;
         tile_of(ic, r0, nt);
+        if constexpr (SKIN) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int b = (r0 + wave * RW + 16 * i) >> 4;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int v = nt * BN + 16 * j + (lane & 15);
+                    const f32x4 t = acc[i][j];
+                    const float x = fmaf(t[0], vpr[i][j][0], fmaf(t[1], vpr[i][j][1], fmaf(t[2], vpr[i][j][2], t[3])));
+                    float* dst = g < 3 && b * 16 < a.M && v < a.Nc ? a.out + (size_t)b * a.ldo + 3 * v + g : a.trash + lane;
+                    *dst = x + tb[i];
+                    acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            return;
+        }
         const int col = nt * BN + cl;
         // bv, xi, xr: loaded by load_epi at the start of the tile's last K step (EARLY) or now
         if constexpr (!EARLY) load_epi(ic);
@@ -1010,10 +1052,14 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st) {
+hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int epi) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     const int kall = xgemm_kmain(a);
-    if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || !a.bias || a.ldo % 4 || a.Nc % bn || a.nseg < 1 || a.nseg > 2 ||
+    const bool skin = epi == EPI_SKIN;
+    if (epi != EPI_BIAS && !skin) return hipErrorInvalidValue;
+    if (skin && (bn != 128 || a.M % 16 || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx))
+        return hipErrorInvalidValue;
+    if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || !a.bias || (!skin && (a.ldo % 4 || a.Nc % bn)) || a.nseg < 1 || a.nseg > 2 ||
         kall < 2 || a.ksplit > 1 || (a.nw != 0 && a.nw != 4))
         return hipErrorInvalidValue;
     for (int s = 0; s <= a.nseg; ++s) {
@@ -1024,19 +1070,21 @@ hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st) {
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
     if (a.rx && (bn != 64 || a.Nc != bn || a.rxc < 0 || a.rxc > 4 || !a.rw || a.idn.src)) return hipErrorInvalidValue;
-    if ((long long)a.M * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
-    const long long ntot = (long long)((a.M + 127) / 128) * (a.Nc / bn);
+    if ((long long)(skin ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
+    const long long ntot = (long long)((a.M + 127) / 128) * ((a.Nc + bn - 1) / bn);
     long long G = std::min<long long>(ntot, 2LL * ncu);
     if (G > 8) G &= ~7LL;   // a multiple of 8: tile id b + i G stays on the workgroup's XCD
     (void)hipGetLastError();
     const dim3 grid((unsigned)G), blk(256);
-    if (bn == 128) {
-        if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<128, true, false>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((xgemm_pt_kernel<128, false, false>), grid, blk, 0, st, a);
+    if (skin) {
+        hipLaunchKernelGGL((xgemm_pt_kernel<128, EPI_SKIN, false, false>), grid, blk, 0, st, a);
+    } else if (bn == 128) {
+        if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<128, EPI_BIAS, true, false>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((xgemm_pt_kernel<128, EPI_BIAS, false, false>), grid, blk, 0, st, a);
     } else {
-        if (a.rx) hipLaunchKernelGGL((xgemm_pt_kernel<64, false, true>), grid, blk, 0, st, a);
-        else if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<64, true, false>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((xgemm_pt_kernel<64, false, false>), grid, blk, 0, st, a);
+        if (a.rx) hipLaunchKernelGGL((xgemm_pt_kernel<64, EPI_BIAS, false, true>), grid, blk, 0, st, a);
+        else if (a.idn.src) hipLaunchKernelGGL((xgemm_pt_kernel<64, EPI_BIAS, true, false>), grid, blk, 0, st, a);
+        else hipLaunchKernelGGL((xgemm_pt_kernel<64, EPI_BIAS, false, false>), grid, blk, 0, st, a);
     }
     return hipGetLastError();
 }

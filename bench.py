@@ -281,6 +281,20 @@ def main():
             b[0] += ms.value; b[1] += 1; b[2] += fl.value; b[3] += by.value
         lib.tik_model_profile(h, 0)
 
+    # N > 1: the gathered poses of the last step are checked on rank 0 against
+    # its own solve of every rank's windows (the inputs are seeded per rank)
+    gather_check = None
+    if world > 1:
+        with torch.no_grad():
+            step()
+            gathers.drain()
+            if rank == 0:
+                xs = torch.from_numpy(np.concatenate([syn.synthetic_windows(B, T, seed=0, start=r * B)
+                                                      for r in range(world)])).to(dev)
+                ref = reg(xs)["poses"]
+                gather_check = {"max_abs_diff_vs_rank0_solve": float((full - ref).abs().max().item()),
+                                "windows": int(world * B)}
+        dist.barrier()
     ms_step = dt / args.steps * 1e3
     value = world * B / (dt / args.steps)
     others = []
@@ -377,6 +391,8 @@ def main():
         }
         if others:
             out["other_precisions"] = others
+        if gather_check is not None:
+            out["gather_check"] = gather_check
         out["profiled_ms_per_step"] = round(dt_prof / args.steps * 1e3, 4)
         out["timing"] = ("value/ms_per_step: K steps with no instrumentation; roofline/forward: a second pass of "
                          "the same K steps with HIP events around every launch on its stream")

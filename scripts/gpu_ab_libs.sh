@@ -22,6 +22,6 @@ fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in "$@"; do
     env $(envs $v) TIK_LIB=$(lib $v) timeout -k 10 200 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-compare > $O/$v$r.json 2> $O/$v$r.err || exit 1
-    python -c "import json;d=json.load(open('$O/$v$r.json'));l=d['forward']['launches'];print('$v$r', d['value'], d['ms_per_step'], 'prof', d['profiled_ms_per_step'], ' '.join(f'{k}={v[\"avg_ms\"]}' for k,v in sorted(l.items()) if k.startswith('XT') or k.startswith('XP') or k.startswith('XG128.L3')))"
+    python -c "import json;d=json.load(open('$O/$v$r.json'));l=d['forward']['launches'];print('$v$r', d['value'], d['ms_per_step'], 'prof', d['profiled_ms_per_step'], ' '.join(f'{k}={v[\"avg_ms\"]}' for k,v in sorted(l.items()) if k.startswith('XG')))"
   done
 done

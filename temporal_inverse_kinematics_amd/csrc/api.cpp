@@ -233,6 +233,7 @@ struct Layer {
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
+    int xnwg = 4;           // the same for the graph (G) launches (TIK_XNWG; TIK_XNW sets both)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int ncu = 256;          // compute units (persistent grid size)
@@ -402,7 +403,7 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune(); g.nw = xnw; g.stagger = xstagger();
+            g.tune = xtune(); g.nw = xnwg; g.stagger = xstagger();
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
@@ -908,7 +909,9 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
     if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
     if (const char* e = getenv("TIK_XNW"))
-        for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
+        for (auto& L : md->layers) L.xnw = L.xnwg = atoi(e) == 8 ? 8 : 4;
+    if (const char* e = getenv("TIK_XNWG"))   // bit mask of layers whose G runs 8 waves (one 255-row workgroup per CU)
+        for (auto& L : md->layers) L.xnwg = (atoi(e) >> L.index) & 1 ? 8 : 4;
     if (const char* e = getenv("TIK_XEPI"))
         for (auto& L : md->layers) L.xepi = atoi(e);
     {

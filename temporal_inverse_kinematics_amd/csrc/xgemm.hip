@@ -62,6 +62,23 @@ __device__ __forceinline__ void xsplit8(const f32x4 lo, const f32x4 hi, xbf16x8&
     }
 }
 
+// epilogue stores of output tiles; a -DTIK_XNT build makes them nontemporal
+// (same-box A/B experiment: the layer outputs are re-read by the next launch)
+__device__ __forceinline__ void xst4(float* p, const f32x4 v) {
+#ifdef TIK_XNT
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#else
+    *reinterpret_cast<f32x4*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void xst1(float* p, const float v) {
+#ifdef TIK_XNT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ int xa_swz(int r) { return (r >> 1) & 7; }
 
 // graph mix of one frame, output joints [W0, W1): z[w] = sum_v A[v][w] y[v] +
@@ -91,7 +108,7 @@ __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&a
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-        *reinterpret_cast<f32x4*>(o + (size_t)w * ldo) = z;
+        xst4(o + (size_t)w * ldo, z);
     }
 }
 
@@ -447,6 +464,10 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             }
         }
     }
+#ifdef TIK_XPRIO
+    // A/B experiment: the epilogue's memory ops ahead of the co-resident workgroup's K loop
+    __builtin_amdgcn_s_setprio(TIK_XPRIO);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tr) t3 = __builtin_amdgcn_s_memtime();
     auto trace_out = [&]() __attribute__((always_inline)) {
@@ -514,7 +535,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 }
                 if (lr < RT && r0 + lr < a.M) {
                     if (cok) {
-                        *reinterpret_cast<f32x4*>(outp + (size_t)(r0 + lr) * a.ldo + col) = v;
+                        xst4(outp + (size_t)(r0 + lr) * a.ldo + col, v);
                     } else {
                         for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
                             float t = *(Cs + lr * LDC + cl + e) + (a.bias ? a.bias[col + e] : 0.f);
@@ -583,7 +604,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                         v[e] += xr[i][0] * rw[e][0] + xr[i][1] * rw[e][1] + xr[i][2] * rw[e][2] + xr[i][3] * rw[e][3];
                         v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                     }
-                    if (rok[i]) *reinterpret_cast<f32x4*>(outp + (size_t)rows[i] * a.ldo + col) = v;
+                    if (rok[i]) xst4(outp + (size_t)rows[i] * a.ldo + col, v);
                 }
             } else {
 #pragma unroll
@@ -916,7 +937,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                     const f32x4 t = acc[i][j];
                     const float x = fmaf(t[0], vpr[i][j][0], fmaf(t[1], vpr[i][j][1], fmaf(t[2], vpr[i][j][2], t[3])));
                     float* dst = g < 3 && b * 16 < a.M && v < a.Nc ? a.out + (size_t)b * a.ldo + 3 * v + g : a.trash + lane;
-                    *dst = x + tb[i];
+                    xst1(dst, x + tb[i]);
                     acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 }
             }
@@ -951,7 +972,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                     v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                 }
                 float* dst = row < a.M ? a.out + (size_t)row * a.ldo + col : a.trash + cl;
-                *reinterpret_cast<f32x4*>(dst) = v;
+                xst4(dst, v);
             }
         }
 #pragma unroll

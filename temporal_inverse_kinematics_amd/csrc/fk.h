@@ -15,7 +15,8 @@ struct FkChainArgs {
     const float* jt;         // (55,3)        J_regressor . v_template
     const float* jd;         // (55,3,nb+ne)  J_regressor . [shapedirs | exprdirs]
     float* feat;             // (B,kp)  [vec(R_j - I), j=1..54 | betas | expr | 1 | 0..]  (fp32 GEMM path; or null)
-    float* ablk;             // (B,16,kj) rows e = 4r+c of A_j (3x4), cols j                (fp32 GEMM path; or null)
+    float* ablk;             // (B,arows,kj) rows e = 4r+c of A_j (3x4), cols j                (fp32 GEMM path; or null)
+    int arows;               // rows of ablk per body: 16 (rows 12..15 = [0 0 0 1]) or 12 (the 3x4 part only)
     unsigned short* feat_sb; // (B, kp/32 blocks of [hi x32 | lo x32]): feat split for the f16x3 GEMM (or null)
     unsigned short* ablk_sb; // (B*16, kj/32 blocks): ablk split likewise (or null)
     float* joints;           // (B,njoints,3): first 55 written here

@@ -155,8 +155,9 @@ __global__ __launch_bounds__(64 * FKW) void fk_chain_kernel(FkChainArgs a) {
     if (!live) return;   // no barrier below
     // (4) outputs: lane j holds column j of A (kj = 64 columns)
     if (a.ablk) {
-        float* G = a.ablk + (size_t)b * 16 * a.kj;
-        for (int e = 0; e < 16; ++e)
+        const int ar = a.arows == 12 ? 12 : 16;
+        float* G = a.ablk + (size_t)b * ar * a.kj;
+        for (int e = 0; e < ar; ++e)
             if (j < a.kj) G[e * a.kj + j] = A[e];
     }
     if (a.ablk_sb) {   // rows b*16+e, K = joint: block j/32, hi at j%32, lo 32 further

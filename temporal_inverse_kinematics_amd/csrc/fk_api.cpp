@@ -41,6 +41,7 @@ struct tik_fk {
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
     DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the skinning GEMM, EPI_SKIN)
     bool xpt = true;   // skinning on the persistent xgemm kernel (TIK_FK_PT=0: one workgroup per tile)
+    bool skin12 = false;  // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=1; under test)
     int ncu = 256;
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
@@ -182,6 +183,7 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         return rc;
     }
     if (const char* e = getenv("TIK_FK_PT")) fk->xpt = e[0] != '0';
+    if (const char* e = getenv("TIK_FK_SKIN12")) fk->skin12 = e[0] != '0';
     {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
@@ -255,6 +257,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     c.pose = full_pose; c.betas = betas; c.expr = expression; c.transl = transl; c.pose_mean = fk->pose_mean.p;
     c.parents = fk->parents.p; c.chain = fk->chain.p; c.jt = fk->jt.p; c.jd = fk->jd.p;
     c.feat = f16x3 ? nullptr : fk->feat.p; c.ablk = f16x3 ? nullptr : fk->ablk.p;
+    // rows of A_j per body in ablk: the persistent bf16x3 skinning GEMM skips the [0 0 0 1] row
+    const int ar = fk->prec == tik::PREC_BF16X3 && fk->xWT.p && fk->xpt && fk->skin12 ? 12 : 16;
+    c.arows = ar;
     c.feat_sb = f16x3 ? fk->feat_sb.p : nullptr; c.ablk_sb = f16x3 ? fk->ablk_sb.p : nullptr;
     c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
     c.depth = fk->depth.p; c.maxdepth = fk->maxdepth;
@@ -296,9 +301,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         if (fk->prec == tik::PREC_BF16X3 && fk->xWT.p) {
             // skinning + vertex transform on xgemm.hip (EPI_SKIN)
             tik::XArgs s{};
-            s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
-            s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * 16, (long long)B * 16};
-            s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s);
+            s.M = B * ar; s.Nc = fk->V; s.V = 1; s.tout = B * ar;
+            s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * ar, (long long)B * ar};
+            s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s); s.skin_rows = ar;
             s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl; s.act = tik::ACT_NONE;
             if (fk->xpt) {   // persistent: the DMA pipeline runs across tiles (K = 64 is 2 steps per tile)
                 s.bias = transl ? transl : fk->zero_transl.p;

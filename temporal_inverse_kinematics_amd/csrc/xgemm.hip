@@ -81,6 +81,20 @@ __device__ __forceinline__ void xst1(float* p, const float v) {
 
 __device__ __forceinline__ int xa_swz(int r) { return (r >> 1) & 7; }
 
+// EPI_SKIN: body b and transform row k of a lane's 4 GEMM rows rb .. rb + 3
+// (rb % 4 == 0, so they never straddle bodies). 16 rows per body: k == 3 is
+// the [0 0 0 1] row (not stored); 12 rows per body: the 3x4 part only
+__device__ __forceinline__ void xskin_row(int rb, int srows, int& b, int& k) {
+    const int q = rb >> 2;
+    if (srows == 12) {
+        b = q / 3;
+        k = q - 3 * b;
+    } else {
+        b = q >> 2;
+        k = q & 3;
+    }
+}
+
 // graph mix of one frame, output joints [W0, W1): z[w] = sum_v A[v][w] y[v] +
 // bias2[w], ReLU, stored. w and v are compile-time, so the sparse COCO
 // pattern unrolls and the A entries are wave-uniform scalar loads.
@@ -871,14 +885,16 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         int r0, nt;
         tile_of(ic, r0, nt);
         if constexpr (SKIN) {
-            // row block of fragment i = body (r0 + 32 wave + 16 i) / 16; lane = vertex
-            // n0 + 16 j + (lane & 15), transform row g (g == 3 and rows / vertices past
+            // lane = vertex n0 + 16 j + (lane & 15), rows r0 + 32 wave + 16 i + 4 g .. +3
+            // = transform row k of body b (xskin_row; k == 3 and rows / vertices past
             // the end load valid dummies and store to a_trash)
+            const int sr = a.skin_rows == 12 ? 12 : 16, nbody = a.M / sr;
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const int b = (r0 + wave * RW + 16 * i) >> 4;
-                const int bb = b * 16 < a.M ? b : 0;
-                tb[i] = a.bias[bb * 3 + (g < 3 ? g : 0)];
+                int b, k;
+                xskin_row(r0 + wave * RW + 16 * i + 4 * g, sr, b, k);
+                const int bb = b < nbody ? b : 0;
+                tb[i] = a.bias[bb * 3 + (k < 3 ? k : 0)];
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     const int v = nt * BN + 16 * j + (lane & 15);
@@ -928,15 +944,17 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         int r0, nt;
         tile_of(ic, r0, nt);
         if constexpr (SKIN) {
+            const int sr = a.skin_rows == 12 ? 12 : 16, nbody = a.M / sr;
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-                const int b = (r0 + wave * RW + 16 * i) >> 4;
+                int b, k;
+                xskin_row(r0 + wave * RW + 16 * i + 4 * g, sr, b, k);
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     const int v = nt * BN + 16 * j + (lane & 15);
                     const f32x4 t = acc[i][j];
                     const float x = fmaf(t[0], vpr[i][j][0], fmaf(t[1], vpr[i][j][1], fmaf(t[2], vpr[i][j][2], t[3])));
-                    float* dst = g < 3 && b * 16 < a.M && v < a.Nc ? a.out + (size_t)b * a.ldo + 3 * v + g : a.trash + lane;
+                    float* dst = k < 3 && b < nbody && v < a.Nc ? a.out + (size_t)b * a.ldo + 3 * v + k : a.trash + lane;
                     xst1(dst, x + tb[i]);
                     acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 }
@@ -1078,7 +1096,9 @@ hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int 
     const int kall = xgemm_kmain(a);
     const bool skin = epi == EPI_SKIN;
     if (epi != EPI_BIAS && !skin) return hipErrorInvalidValue;
-    if (skin && (bn != 128 || a.M % 16 || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx))
+    if (skin && (a.skin_rows != 0 && a.skin_rows != 12 && a.skin_rows != 16)) return hipErrorInvalidValue;
+    const int srows = skin && a.skin_rows == 12 ? 12 : 16;
+    if (skin && (bn != 128 || a.M % srows || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx))
         return hipErrorInvalidValue;
     if ((bn != 64 && bn != 128) || !a.wp || !a.out || !a.trash || !a.bias || (!skin && (a.ldo % 4 || a.Nc % bn)) || a.nseg < 1 || a.nseg > 2 ||
         kall < 2 || a.ksplit > 1 || (a.nw != 0 && a.nw != 4))
@@ -1091,7 +1111,7 @@ hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int 
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
     if (a.rx && (bn != 64 || a.Nc != bn || a.rxc < 0 || a.rxc > 4 || !a.rw || a.idn.src)) return hipErrorInvalidValue;
-    if ((long long)(skin ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
+    if ((long long)(skin ? a.M / srows : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const long long ntot = (long long)((a.M + 127) / 128) * ((a.Nc + bn - 1) / bn);
     long long G = std::min<long long>(ntot, 2LL * ncu);
     if (G > 8) G &= ~7LL;   // a multiple of 8: tile id b + i G stays on the workgroup's XCD
@@ -1130,7 +1150,7 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.rx && (bn != 64 || epi != EPI_BIAS || a.rxc < 0 || a.rxc > 4)) return hipErrorInvalidValue;
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
-    if (epi == EPI_SKIN && (a.M % 16 || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx || a.nw == 8))
+    if (epi == EPI_SKIN && (a.M % 16 || (a.skin_rows && a.skin_rows != 16) || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx || a.nw == 8))
         return hipErrorInvalidValue;
     if ((long long)(epi == EPI_SKIN ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const int nw = a.nw == 8 ? 8 : 4, rt = xgemm_tile_rows(epi, nw);

@@ -106,6 +106,26 @@ def test_fk_config4_full_batch(consts, model):
         assert torch.equal(v[i:i + 1], v1) and torch.equal(j[i:i + 1], j1)
 
 
+@pytest.mark.parametrize("B", [1, 37, 301])
+def test_fk_skin12_layout_bitwise(consts, monkeypatch, B):
+    """The persistent bf16x3 skinning GEMM on 12 rows per body (TIK_FK_SKIN12=1:
+    only the 3x4 part of A_j, so 16-row fragments straddle bodies and row
+    tiles end mid-body) gives the 16-row layout's vertices and joints bit for
+    bit: every output element is the same K-ordered dot product."""
+    from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
+    pose, betas, expr, transl = _inputs(B, 70 + B)
+    cu = lambda a: torch.from_numpy(a).cuda()
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("TIK_FK_SKIN12", flag)
+        m = SMPLX(consts, batch_size=9, precision="bf16x3")
+        outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), cu(transl)))
+    (j16, v16), (j12, v12) = outs
+    assert torch.equal(v16, v12) and torch.equal(j16, j12)
+    _, vr = sl.smplx_forward(consts, pose[-1:], betas[-1:], expr[-1:], transl[-1:])
+    assert np.abs(v12[-1:].cpu().numpy() - vr).max() < TOL
+
+
 def _write_smplx_npz(path, c):
     """The constants in the SMPL-X model-file layout (the keys and shapes of
     SMPLX_{MALE,FEMALE,NEUTRAL}.npz as smplx.body_models.SMPLX reads them)."""

@@ -41,7 +41,7 @@ struct tik_fk {
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
     DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the skinning GEMM, EPI_SKIN)
     bool xpt = true;   // skinning on the persistent xgemm kernel (TIK_FK_PT=0: one workgroup per tile)
-    bool skin12 = false;  // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=1; under test)
+    bool skin12 = true;   // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=0: 16)
     int ncu = 256;
     int prec = 1;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;

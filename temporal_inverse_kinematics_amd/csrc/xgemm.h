@@ -51,6 +51,7 @@ struct XArgs {
     int ldr;
     float* out;                 // fp32 [M][ldo]
     float* trash;               // xgemm_pt: >= BN floats, the store target of rows past M
+    int nts;                    // nontemporal output stores (EPI_BIAS / EPI_GRAPH; the backbone's layer outputs)
     int skin_rows;              // EPI_SKIN on xgemm_pt: GEMM rows per body, 16 (A_j rows 4r+c incl. [0 0 0 1]; 0 = 16) or 12 (3x4 only)
     int ldo;
     int act;

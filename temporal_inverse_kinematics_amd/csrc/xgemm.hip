@@ -62,21 +62,12 @@ __device__ __forceinline__ void xsplit8(const f32x4 lo, const f32x4 hi, xbf16x8&
     }
 }
 
-// epilogue stores of output tiles; a -DTIK_XNT build makes them nontemporal
-// (same-box A/B experiment: the layer outputs are re-read by the next launch)
-__device__ __forceinline__ void xst4(float* p, const f32x4 v) {
-#ifdef TIK_XNT
-    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-#else
-    *reinterpret_cast<f32x4*>(p) = v;
-#endif
-}
-__device__ __forceinline__ void xst1(float* p, const float v) {
-#ifdef TIK_XNT
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
+// epilogue stores of output tiles: nontemporal for the backbone's layer
+// outputs (XArgs::nts; same-box A/B +0.9 % IK frames/s), plain for split-K
+// partials and the FK GEMMs (re-read at once; NT measured slower there)
+__device__ __forceinline__ void xst4(float* p, const f32x4 v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    else *reinterpret_cast<f32x4*>(p) = v;
 }
 
 __device__ __forceinline__ int xa_swz(int r) { return (r >> 1) & 7; }
@@ -108,7 +99,7 @@ __device__ __forceinline__ float xam(const float (&amv)[5], int i) {
 template <int W0, int W1, bool SPARSE, int BN>
 __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&amv)[5],
                                            const float* __restrict__ bias2s, int lcol, float* __restrict__ o,
-                                           int ldo) {
+                                           int ldo, bool nt) {
 #pragma unroll
     for (int w = W0; w < W1; ++w) {
         f32x4 z = *reinterpret_cast<const f32x4*>(bias2s + w * BN + lcol);
@@ -122,7 +113,7 @@ __device__ __forceinline__ void xmix_store(const f32x4 (&y)[17], const float (&a
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-        xst4(o + (size_t)w * ldo, z);
+        xst4(o + (size_t)w * ldo, z, nt);
     }
 }
 
@@ -478,10 +469,6 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             }
         }
     }
-#ifdef TIK_XPRIO
-    // A/B experiment: the epilogue's memory ops ahead of the co-resident workgroup's K loop
-    __builtin_amdgcn_s_setprio(TIK_XPRIO);
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tr) t3 = __builtin_amdgcn_s_memtime();
     auto trace_out = [&]() __attribute__((always_inline)) {
@@ -549,7 +536,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 }
                 if (lr < RT && r0 + lr < a.M) {
                     if (cok) {
-                        xst4(outp + (size_t)(r0 + lr) * a.ldo + col, v);
+                        xst4(outp + (size_t)(r0 + lr) * a.ldo + col, v, a.nts);
                     } else {
                         for (int e = 0; e < 4 && col + e < a.Nc; ++e) {
                             float t = *(Cs + lr * LDC + cl + e) + (a.bias ? a.bias[col + e] : 0.f);
@@ -618,7 +605,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                         v[e] += xr[i][0] * rw[e][0] + xr[i][1] * rw[e][1] + xr[i][2] * rw[e][2] + xr[i][3] * rw[e][3];
                         v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                     }
-                    if (rok[i]) xst4(outp + (size_t)rows[i] * a.ldo + col, v);
+                    if (rok[i]) xst4(outp + (size_t)rows[i] * a.ldo + col, v, a.nts);
                 }
             } else {
 #pragma unroll
@@ -707,11 +694,11 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
             for (int v = 0; v < 17; ++v) y[v] = *reinterpret_cast<const f32x4*>(Cs + (f * 17 + v) * C::LDCG + 4 * c4);
             float* o = a.out + (size_t)(f0 + f) * 17 * a.ldo + col;
             if (a.mix_sparse) {
-                if (second) xmix_store<9, 17, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
-                else xmix_store<0, 9, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
+                if (second) xmix_store<9, 17, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo, a.nts);
+                else xmix_store<0, 9, true, BN>(y, amv, b2s, 4 * c4, o, a.ldo, a.nts);
             } else {
-                if (second) xmix_store<9, 17, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
-                else xmix_store<0, 9, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo);
+                if (second) xmix_store<9, 17, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo, a.nts);
+                else xmix_store<0, 9, false, BN>(y, amv, b2s, 4 * c4, o, a.ldo, a.nts);
             }
         }
     }
@@ -955,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                     const f32x4 t = acc[i][j];
                     const float x = fmaf(t[0], vpr[i][j][0], fmaf(t[1], vpr[i][j][1], fmaf(t[2], vpr[i][j][2], t[3])));
                     float* dst = k < 3 && b < nbody && v < a.Nc ? a.out + (size_t)b * a.ldo + 3 * v + k : a.trash + lane;
-                    xst1(dst, x + tb[i]);
+                    *dst = x + tb[i];
                     acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 }
             }
@@ -990,7 +977,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                     v[e] = v[e] > 0.f ? v[e] : slope * v[e];
                 }
                 float* dst = row < a.M ? a.out + (size_t)row * a.ldo + col : a.trash + cl;
-                xst4(dst, v);
+                xst4(dst, v, a.nts);
             }
         }
 #pragma unroll

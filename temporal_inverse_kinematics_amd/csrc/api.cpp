@@ -133,10 +133,11 @@ static int xstagger() {
     static const int v = [] { const char* e = getenv("TIK_XSTAGGER"); return e ? atoi(e) : 0; }();
     return v;
 }
-// nontemporal stores of the backbone's layer outputs (XArgs::nts), TIK_XNTS=0 turns them off
-static int xnts() {
-    static const int v = [] { const char* e = getenv("TIK_XNTS"); return e && e[0] == '0' ? 0 : 1; }();
-    return v;
+// nontemporal stores of the backbone's layer outputs (XArgs::nts): TIK_XNTS = bit mask of
+// the layers that use them (default all; 0 = none)
+static int xnts(int layer) {
+    static const int m = [] { const char* e = getenv("TIK_XNTS"); return e ? atoi(e) : 255; }();
+    return (m >> layer) & 1;
 }
 // tuning experiments on the xgemm kernels (XArgs::tune), TIK_XTUNE=<bits>; 0 in production
 int xtune() {
@@ -408,7 +409,7 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune(); g.nw = xnwg; g.stagger = xstagger(); g.nts = xnts();
+            g.tune = xtune(); g.nw = xnwg; g.stagger = xstagger(); g.nts = xnts(index);
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
@@ -435,7 +436,7 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger(); t.nts = xnts();
+        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger(); t.nts = xnts(index);
         const bool pt = xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
         const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);

@@ -132,26 +132,28 @@ def _cpu_model():
 def _cpu_baseline(T: int, seconds: float = 12.0):
     """The reference forward restated with the torch CPU ops the reference runs
     (oracle/stgcn.py pose_regressor_torch, pinned to the reference's fixtures),
-    fp32, eval, on a bounded sample. Thread count: the best of the CPUs this
-    process may run on (sched_getaffinity) and the box's 16-CPU share, probed
-    briefly; the count used is reported."""
+    fp32, eval, on a bounded sample, in batches of 64 windows (the reference's
+    inference batch, inference.py:43). Thread count: 16, 32, 64, 128 and 256
+    (those the process may run on, sched_getaffinity) probed on one batch each;
+    the fastest is used and reported with every probe's rate."""
     import numpy as np
     import torch
 
     from oracle import stgcn as orc
     from temporal_inverse_kinematics_amd import synthetic as syn
     sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
-    nb = 16
+    nb = 64
     x = syn.synthetic_windows(nb, T, seed=7)
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cands = sorted({max(1, min(16, avail)), avail})
-    best, rate = cands[0], 0.0
+    cands = sorted({n for n in (16, 32, 64, 128, 256) if n <= avail} | {min(16, avail)})
+    best, rate, probes = cands[0], 0.0, {}
     for n in cands:
         torch.set_num_threads(n)
-        orc.pose_regressor_torch(x[:2], sd)
+        orc.pose_regressor_torch(x[:4], sd)
         t0 = time.perf_counter()
         orc.pose_regressor_torch(x, sd)
         r = nb / (time.perf_counter() - t0)
+        probes[str(n)] = round(r, 1)
         if r > rate:
             best, rate = n, r
     torch.set_num_threads(best)
@@ -162,7 +164,7 @@ def _cpu_baseline(T: int, seconds: float = 12.0):
     dt = time.perf_counter() - t0
     return {"value": round(done / dt, 1), "unit": "IK frames/s", "cores": int(best), "kind": "port",
             "cpu_model": _cpu_model(), "visible_cpus": os.cpu_count(), "affinity_cpus": avail,
-            "threads_probed": cands,
+            "threads_probed": probes,
             "sample": f"{done} windows (T={T}, batches of {nb}) of the reference forward restated in torch CPU ops "
                       f"(oracle/stgcn.py pose_regressor_torch, fp32 eval, pinned to the reference's fixtures) "
                       f"in {dt:.1f}s on {best} threads"}
@@ -181,6 +183,8 @@ def main():
                     help="GEMM arithmetic: bf16x3 (default; fp32 range, 6 bf16 MFMA products), exact fp32 "
                          "MFMA, or the narrower-range f16x3 split")
     ap.add_argument("--no-compare", action="store_true", help="skip the other-precision comparison runs")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the config #4 (fk) and #5 (online) measurements appended at N=1")
     ap.add_argument("--no-profile", action="store_true",
                     help="diagnostic: no per-launch HIP events in the timed region (no roofline)")
     ap.add_argument("--pmc-traffic", default=None,
@@ -333,10 +337,17 @@ def main():
         # the path is MFMA-bound (~36k FLOP per HBM byte). The roof
         # is the dense peak of the MFMA that executes the products: bf16x3 runs 6
         # bf16 MFMA products per fp32 product, so its fp32-equivalent peak is 2516.6/6
+        # the binding roof of the dominant kernel: the larger of its fractions of
+        # the MFMA roof (algorithmic FLOPs) and of the HBM roof (algorithmic bytes)
         nprod, xpeak, instr = ARITH[args.precision]
-        bound, achieved, peak, unit = "mfma", tflops, xpeak / nprod, "TFLOP/s"
-        basis = (f"{instr} dense peak {xpeak} TF / {nprod} MFMA products per fp32 product = {xpeak / nprod:.1f} "
-                 f"fp32-equivalent TF; achieved = algorithmic fp32 FLOPs (SURVEY.md §8(d)) / HIP-event launch time")
+        if gbs / HBM_PEAK_GBS > tflops / (xpeak / nprod):
+            bound, achieved, peak, unit = "hbm", gbs, HBM_PEAK_GBS, "GB/s"
+            basis = ("HBM3E spec peak; achieved = algorithmic activation bytes (SURVEY.md §8(d)) / HIP-event "
+                     "launch time (its MFMA fraction is lower)")
+        else:
+            bound, achieved, peak, unit = "mfma", tflops, xpeak / nprod, "TFLOP/s"
+            basis = (f"{instr} dense peak {xpeak} TF / {nprod} MFMA products per fp32 product = {xpeak / nprod:.1f} "
+                     f"fp32-equivalent TF; achieved = algorithmic fp32 FLOPs (SURVEY.md §8(d)) / HIP-event launch time")
         traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom, args.precision)
         mfma_busy, mfma_src = _pmc_mfma(args.pmc_mfma, dom, args.precision)
         kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
@@ -396,6 +407,12 @@ def main():
         out["profiled_ms_per_step"] = round(dt_prof / args.steps * 1e3, 4)
         out["timing"] = ("value/ms_per_step: K steps with no instrumentation; roofline/forward: a second pass of "
                          "the same K steps with HIP events around every launch on its stream")
+        if world == 1 and not args.no_extras:
+            # BASELINE configs #4 and #5 under the same clock (the headline stays config #2)
+            from bench_fk import measure_fk
+            from bench_stream import measure_online
+            out["fk"] = measure_fk(batch=4096, steps=10, warmup=3)
+            out["online"] = measure_online(frames=2000, warmup=100, win=T)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = _cpu_baseline(T, args.cpu_seconds)
         print(json.dumps(out))

@@ -269,6 +269,11 @@ int tik_fk_num_verts(tik_fk_t fk);
 int tik_fk_reserve(tik_fk_t fk, int B);
 int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, const float* expression,
                    const float* transl, int B, float* joints, float* verts, void* stream);
+/* Per-launch HIP-event profile of tik_fk_forward (fk_chain, fk_blend, fk_skin,
+ * fk_landmarks), as tik_model_profile / _count / _read. */
+int tik_fk_profile(tik_fk_t fk, int max_launches);
+int tik_fk_profile_count(tik_fk_t fk);
+int tik_fk_profile_read(tik_fk_t fk, int i, char* label, int label_len, float* ms, double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,10 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_fk_num_verts": (_I, (_P,)),
     "tik_fk_reserve": (_I, (_P, _I)),
     "tik_fk_forward": (_I, (_P, _P, _P, _P, _P, _I, _P, _P, _P)),
+    "tik_fk_profile": (_I, (_P, _I)),
+    "tik_fk_profile_count": (_I, (_P,)),
+    "tik_fk_profile_read": (_I, (_P, _I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_float),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double))),
     "tik_trainer_create": (_I, (ctypes.POINTER(TikTensor), _I, ctypes.c_float, ctypes.POINTER(_P))),
     "tik_trainer_destroy": (_I, (_P,)),
     "tik_trainer_step": (_I, (_P, _P, _I, _I, _P, _P, ctypes.c_ulonglong, _P, _P)),

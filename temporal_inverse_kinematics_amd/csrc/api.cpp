@@ -128,11 +128,6 @@ hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, co
     return e;
 }
 
-// desync experiment on the xgemm kernels (XArgs::stagger), TIK_XSTAGGER=<n>; 0 in production
-static int xstagger() {
-    static const int v = [] { const char* e = getenv("TIK_XSTAGGER"); return e ? atoi(e) : 0; }();
-    return v;
-}
 // nontemporal stores of the backbone's layer outputs (XArgs::nts): TIK_XNTS = bit mask of
 // the layers that use them (default all; 0 = none)
 static int xnts(int layer) {
@@ -145,45 +140,6 @@ int xtune() {
     return t;
 }
 
-// Optional per-launch HIP-event profiler (bench.py's roofline numbers): one
-// event pair per kernel launch on the launch stream, algorithmic FLOPs and
-// bytes computed from the shapes.
-struct Profiler {
-    struct Rec {
-        std::string label;
-        double flops, bytes;
-    };
-    std::vector<hipEvent_t> ev0, ev1;
-    std::vector<Rec> recs;
-    int cap = 0;
-    ~Profiler() { clear(); }
-    void clear() {
-        for (auto e : ev0) (void)hipEventDestroy(e);
-        for (auto e : ev1) (void)hipEventDestroy(e);
-        ev0.clear(); ev1.clear(); recs.clear(); cap = 0;
-    }
-    int enable(int n) {
-        clear();
-        for (int i = 0; i < n; ++i) {
-            hipEvent_t a, b;
-            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
-                return fail(TIK_E_HIP, "hipEventCreate failed");
-            ev0.push_back(a); ev1.push_back(b);
-        }
-        cap = n;
-        return TIK_OK;
-    }
-    int begin(const char* label, double flops, double bytes, hipStream_t st) {
-        if ((int)recs.size() >= cap) return -1;
-        const int i = (int)recs.size();
-        recs.push_back({label, flops, bytes});
-        (void)hipEventRecord(ev0[i], st);
-        return i;
-    }
-    void end(int i, hipStream_t st) {
-        if (i >= 0) (void)hipEventRecord(ev1[i], st);
-    }
-};
 thread_local Profiler* g_prof = nullptr;   // set for the duration of a profiled call
 
 // debug (TIK_CHECKSUM=1): after every annotated launch, synchronise and
@@ -239,7 +195,6 @@ struct Layer {
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
-    int xnwg = 4;           // the same for the graph (G) launches (TIK_XNWG; TIK_XNW sets both)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int ncu = 256;          // compute units (persistent grid size)
@@ -395,7 +350,7 @@ struct Layer {
     // ([rows][4]) for the residual conv in the temporal conv's epilogue.
     int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st,
                   const float* xraw = nullptr, const float* bn_sc = nullptr, const float* bn_sh = nullptr,
-                  float* xb4 = nullptr, hipEvent_t ev_g = nullptr) const {
+                  float* xb4 = nullptr) const {
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         const double px_in = (double)rin, px_out = (double)rout;
@@ -409,14 +364,13 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune(); g.nw = xnwg; g.stagger = xstagger(); g.nts = xnts(index);
+            g.tune = xtune(); g.nw = xnw; g.nts = xnts(index);
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
-        if (ev_g) HIP_TRY(hipEventRecord(ev_g, st));   // split-batch lag point (backbone_x)
         tik::XArgs t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
         t.seg[0] = tik::XSeg{z, cout, cout, TK, stride, 1, tin, rin};
@@ -436,7 +390,7 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.stagger = xstagger(); t.nts = xnts(index);
+        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.nts = xnts(index);
         const bool pt = xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
         const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) + std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
@@ -752,7 +706,6 @@ struct tik_model {
     hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT - 1] = {};
     bool split = true;                 // TIK_SPLIT=0: one stream
     int nsplit = 2;                    // parts of a split batch (TIK_SPLIT_N, 2..4)
-    int split_lag = 0;                 // xgemm path: parts 1.. start after part 0's launch number split_lag (TIK_SPLIT_LAG)
     std::atomic<int> refs{1};          // the handle + every live online-IK stream
     ~tik_model() {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -783,6 +736,41 @@ struct tik_block {
     DevBuf xp, z;   // padded-input and z workspace
     int prec = 1;
 };
+
+// handle settings read from the environment (A/B and test hooks) and the
+// device facts the launches need; the same for full and backbone-only handles
+static void apply_env(tik_model* md) {
+    if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
+    if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
+    if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
+    if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
+    if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
+    if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
+    if (const char* e = getenv("TIK_XNW"))
+        for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
+    if (const char* e = getenv("TIK_XEPI"))
+        for (auto& L : md->layers) L.xepi = atoi(e);
+    {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+            for (auto& L : md->layers) L.ncu = ncu;
+        const char* e = getenv("TIK_XPT");
+        for (auto& L : md->layers) {
+            // default: the 64-column temporal convs (6 K steps per tile: the
+            // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
+            L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
+            L.xtrash = reinterpret_cast<float*>(md->trash.p);
+        }
+    }
+    if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
+    if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
+    if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
+    if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
+        if (!strcmp(e, "dma")) md->dma_min_frames = 1;
+        else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
+    }
+    if (const char* e = getenv("TIK_XHEAD_KS")) md->xhead_ks = std::min(8, atoi(e));
+}
 
 extern "C" {
 
@@ -895,6 +883,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
             delete md;
             return rc;
         }
+        apply_env(md);
         *out = md;
         return TIK_OK;
     }
@@ -908,38 +897,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         delete md;
         return rc;
     }
-    if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
-    if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
-    if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
-    if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
-    if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
-    if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
-    if (const char* e = getenv("TIK_XNW"))
-        for (auto& L : md->layers) L.xnw = L.xnwg = atoi(e) == 8 ? 8 : 4;
-    if (const char* e = getenv("TIK_XNWG"))   // bit mask of layers whose G runs 8 waves (one 255-row workgroup per CU)
-        for (auto& L : md->layers) L.xnwg = (atoi(e) >> L.index) & 1 ? 8 : 4;
-    if (const char* e = getenv("TIK_XEPI"))
-        for (auto& L : md->layers) L.xepi = atoi(e);
-    {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
-            for (auto& L : md->layers) L.ncu = ncu;
-        const char* e = getenv("TIK_XPT");
-        for (auto& L : md->layers) {
-            // default: the 64-column temporal convs (6 K steps per tile: the
-            // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
-            L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
-            L.xtrash = reinterpret_cast<float*>(md->trash.p);
-        }
-    }
-    if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
-    if (const char* e = getenv("TIK_SPLIT_LAG")) md->split_lag = std::max(0, atoi(e));
-    if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
-    if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
-    if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
-        if (!strcmp(e, "dma")) md->dma_min_frames = 1;
-        else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
-    }
+    apply_env(md);
     if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
         (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
         (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
@@ -950,7 +908,6 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
         delete md;
         return rc;
     }
-    if (const char* e = getenv("TIK_XHEAD_KS")) md->xhead_ks = std::min(8, atoi(e));
     if (md->feat % 32 == 0) {
         const tik::XPackSeg h{W0->v.data(), md->feat, 1, md->feat};
         if ((rc = md->xh0.upload(tik::xgemm_pack(&h, 1, md->hidden, 128)))) { delete md; return rc; }
@@ -1114,22 +1071,17 @@ static int x_chunk(const tik_model* m, int T) {
 
 // Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
 // from the raw keypoints (data_bn folded into its gcn kernel).
-// ev (split batches, part 0 only): recorded after launch number `lag` of the
-// backbone (G of layer l = launch 2l + 1, its T = 2l + 2), so the other parts
-// start that many launches behind and their G and T launches interleave.
 static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st,
-                      const WsPtrs& w, int lag = 0, hipEvent_t ev = nullptr) {
+                      const WsPtrs& w) {
     const float* cur = nullptr;
     int ld = 0, t = T, rc;
     float* bufs[2] = {w.a0, w.a1};
     int which = 0;
     for (const Layer& L : m->layers) {
         float* o = bufs[which];
-        hipEvent_t eg = ev && lag == 2 * L.index + 1 ? ev : nullptr;
-        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb, eg);
-        else rc = L.forward_x(cur, ld, N, t, w.z, o, st, nullptr, nullptr, nullptr, nullptr, eg);
+        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb);
+        else rc = L.forward_x(cur, ld, N, t, w.z, o, st);
         if (rc) return rc;
-        if (ev && lag == 2 * L.index + 2) HIP_TRY(hipEventRecord(ev, st));
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);
@@ -1383,11 +1335,10 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
         const bool split = allow_split && m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
         const int np = split ? std::min(m->nsplit, std::min(N, chunk)) : 1;
         if (split && (rc = reserve_parts(m, np, (std::min(N, chunk) + np - 1) / np, T))) return rc;
-        const int lag = m->split_lag;
-        auto part = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w, hipEvent_t ev) -> int {
+        auto part = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w) -> int {
             float* fs;
             int r;
-            if ((r = backbone_x(m, xs, n, T, &fs, &to, s, w, lag, ev))) return r;
+            if ((r = backbone_x(m, xs, n, T, &fs, &to, s, w))) return r;
             return head_x(m, fs, n * to, ps, w, s);
         };
         for (int n0 = 0; n0 < N; n0 += chunk) {
@@ -1395,23 +1346,19 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
             const float* xs = x + (size_t)n0 * T * m->V * m->C0;
             float* ps = poses + (size_t)n0 * To * m->pose_dim;
             if (split && n >= np && (long long)n * T >= 32768) {
-                // the other parts start after part 0's launch number `lag`
-                // (0: together, at the fork), so their G and T launches interleave
-                if (lag <= 0) HIP_TRY(hipEventRecord(m->ev_fork, st));
+                HIP_TRY(hipEventRecord(m->ev_fork, st));
+                for (int k = 1; k < np; ++k) HIP_TRY(hipStreamWaitEvent(m->aux[k - 1], m->ev_fork, 0));
                 for (int k = 0; k < np; ++k) {
                     const int a0 = (int)((long long)n * k / np), a1 = (int)((long long)n * (k + 1) / np);
-                    if (k == 1)
-                        for (int j = 1; j < np; ++j) HIP_TRY(hipStreamWaitEvent(m->aux[j - 1], m->ev_fork, 0));
                     if ((rc = part(xs + (size_t)a0 * T * m->V * m->C0, a1 - a0, ps + (size_t)a0 * To * m->pose_dim,
-                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]),
-                                   k == 0 && lag > 0 ? m->ev_fork : nullptr)))
+                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]))))
                         return rc;
                 }
                 for (int k = 1; k < np; ++k) {
                     HIP_TRY(hipEventRecord(m->ev_join[k - 1], m->aux[k - 1]));
                     HIP_TRY(hipStreamWaitEvent(st, m->ev_join[k - 1], 0));
                 }
-            } else if ((rc = part(xs, n, ps, st, ptrs_of(ws), nullptr))) {
+            } else if ((rc = part(xs, n, ps, st, ptrs_of(ws)))) {
                 return rc;
             }
         }
@@ -1463,16 +1410,8 @@ int tik_model_profile_count(tik_model_t m) {
 
 int tik_model_profile_read(tik_model_t m, int i, char* label, int label_len, float* ms, double* flops,
                            double* bytes) {
-    if (!m || i < 0 || i >= (int)m->prof.recs.size()) return fail(TIK_E_INVALID, "tik_model_profile_read: bad index");
-    const auto& r = m->prof.recs[i];
-    if (label && label_len > 0) {
-        strncpy(label, r.label.c_str(), label_len - 1);
-        label[label_len - 1] = 0;
-    }
-    if (flops) *flops = r.flops;
-    if (bytes) *bytes = r.bytes;
-    if (ms) HIP_TRY(hipEventElapsedTime(ms, m->prof.ev0[i], m->prof.ev1[i]));
-    return TIK_OK;
+    if (!m) return fail(TIK_E_INVALID, "tik_model_profile_read: null model");
+    return m->prof.read(i, label, label_len, ms, flops, bytes);
 }
 
 // ---------------------------------------------------------------------------- block API

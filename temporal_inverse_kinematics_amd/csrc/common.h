@@ -247,6 +247,69 @@ struct Workspace {
     DevBuf part;                     // split-K partial sums (small-batch launches)
 };
 
+// Optional per-launch HIP-event profiler (bench.py's roofline numbers): one
+// event pair per kernel launch on the launch stream, algorithmic FLOPs and
+// bytes computed from the shapes.
+struct Profiler {
+    struct Rec {
+        std::string label;
+        double flops, bytes;
+    };
+    std::vector<hipEvent_t> ev0, ev1;
+    std::vector<Rec> recs;
+    int cap = 0;
+    ~Profiler() { clear(); }
+    void clear() {
+        for (auto e : ev0) (void)hipEventDestroy(e);
+        for (auto e : ev1) (void)hipEventDestroy(e);
+        ev0.clear(); ev1.clear(); recs.clear(); cap = 0;
+    }
+    int enable(int n) {
+        clear();
+        for (int i = 0; i < n; ++i) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+                return fail(TIK_E_HIP, "hipEventCreate failed");
+            ev0.push_back(a); ev1.push_back(b);
+        }
+        cap = n;
+        return TIK_OK;
+    }
+    int begin(const char* label, double flops, double bytes, hipStream_t st) {
+        if ((int)recs.size() >= cap) return -1;
+        const int i = (int)recs.size();
+        recs.push_back({label, flops, bytes});
+        (void)hipEventRecord(ev0[i], st);
+        return i;
+    }
+    void end(int i, hipStream_t st) {
+        if (i >= 0) (void)hipEventRecord(ev1[i], st);
+    }
+    // record i's label, HIP-event time and algorithmic work (after the stream synchronised)
+    int read(int i, char* label, int label_len, float* ms, double* flops, double* bytes) const {
+        if (i < 0 || i >= (int)recs.size()) return fail(TIK_E_INVALID, "profile read: bad index %d", i);
+        const auto& r = recs[i];
+        if (label && label_len > 0) {
+            strncpy(label, r.label.c_str(), label_len - 1);
+            label[label_len - 1] = 0;
+        }
+        if (flops) *flops = r.flops;
+        if (bytes) *bytes = r.bytes;
+        if (ms) HIP_TRY(hipEventElapsedTime(ms, ev0[i], ev1[i]));
+        return TIK_OK;
+    }
+};
+
+// one profiled launch: the event pair around the scope (no-op when p is null)
+struct ProfRange {
+    Profiler* p;
+    hipStream_t st;
+    int i;
+    ProfRange(Profiler* p_, const char* label, double flops, double bytes, hipStream_t s)
+        : p(p_), st(s), i(p_ ? p_->begin(label, flops, bytes, s) : -1) {}
+    ~ProfRange() { if (p) p->end(i, st); }
+};
+
 }  // namespace tik_host
 
 struct tik_model;

@@ -54,6 +54,8 @@ struct tik_fk {
     DevBuf zero_transl;   // (B,3) zeros: the skinning kernel always reads a translation
     DevIBuf dyn_bin;
     int cap = 0;
+    Profiler prof;     // per-launch HIP events (tik_fk_profile; bench.py's FK roofline)
+    bool profiling = false;
 };
 
 static const HostTensor* need(const TensorMap& m, const char* k, int& rc) {
@@ -263,7 +265,12 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     c.feat_sb = f16x3 ? fk->feat_sb.p : nullptr; c.ablk_sb = f16x3 ? fk->ablk_sb.p : nullptr;
     c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
     c.depth = fk->depth.p; c.maxdepth = fk->maxdepth;
-    HIP_TRY(tik::launch_fk_chain(c, st));
+    Profiler* pf = fk->profiling ? &fk->prof : nullptr;
+    const double Bd = B, Vd = fk->V;
+    {
+        ProfRange pr(pf, "fk_chain", 0.0, 4.0 * Bd * (NJ * 3 + 20 + KP + 16 * KJ), st);
+        HIP_TRY(tik::launch_fk_chain(c, st));
+    }
 
     const int V3 = 3 * fk->V;
     if (f16x3) {
@@ -287,6 +294,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
             g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
             g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
+            // algorithmic: K = 507 live blend-shape columns (486 pose + 20 shape + template);
+            // bytes: feat rows in, v_posed out, P^T once
+            ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
             HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, st));
         } else {
         tik::CgemmArgs g{};   // v_posed = feat . P
@@ -305,6 +315,10 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * ar, (long long)B * ar};
             s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s); s.skin_rows = ar;
             s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl; s.act = tik::ACT_NONE;
+            // algorithmic: 12 transform entries x 55 joints per (body, vertex) + the
+            // 3x4 vertex transform; bytes: A_j rows and v_posed in, vertices out, W once
+            ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 12 * NJ + 18.0 * Bd * Vd,
+                         4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
             if (fk->xpt) {   // persistent: the DMA pipeline runs across tiles (K = 64 is 2 steps per tile)
                 s.bias = transl ? transl : fk->zero_transl.p;
                 s.trash = reinterpret_cast<float*>(fk->trash.p);
@@ -328,8 +342,27 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     l.verts = vout; l.transl = transl; l.extra = fk->extra.p; l.faces = fk->faces.p; l.lmk_faces = fk->lmk_faces.p;
     l.lmk_bary = fk->lmk_bary.p; l.dyn_faces = fk->dyn_faces.p; l.dyn_bary = fk->dyn_bary.p;
     l.dyn_bin = fk->dyn_bin.p; l.joints = joints;
-    HIP_TRY(tik::launch_fk_landmarks(l, st));
+    {
+        ProfRange pr(pf, "fk_landmarks", 0.0, 4.0 * Bd * (3.0 * 144 + 3.0 * 3 * 3 * 89), st);
+        HIP_TRY(tik::launch_fk_landmarks(l, st));
+    }
     return TIK_OK;
+}
+
+int tik_fk_profile(tik_fk_t fk, int max_launches) {
+    if (!fk || max_launches < 0) return fail(TIK_E_INVALID, "tik_fk_profile: bad arguments");
+    fk->profiling = max_launches > 0;
+    return max_launches > 0 ? fk->prof.enable(max_launches) : (fk->prof.clear(), TIK_OK);
+}
+
+int tik_fk_profile_count(tik_fk_t fk) {
+    if (!fk) return fail(TIK_E_INVALID, "null FK handle");
+    return (int)fk->prof.recs.size();
+}
+
+int tik_fk_profile_read(tik_fk_t fk, int i, char* label, int label_len, float* ms, double* flops, double* bytes) {
+    if (!fk) return fail(TIK_E_INVALID, "tik_fk_profile_read: null FK handle");
+    return fk->prof.read(i, label, label_len, ms, flops, bytes);
 }
 
 }  // extern "C"

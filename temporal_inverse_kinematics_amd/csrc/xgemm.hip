@@ -184,11 +184,6 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         r0 = (swz / gridDim.y) * RT;
         ntile = swz % gridDim.y;
     }
-    if (a.stagger > 0) {   // desynchronise the two workgroups per CU (experiment)
-        const int bid = blockIdx.y * gridDim.x + blockIdx.x;
-        if (bid >= 256 && bid < 512)
-            for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     const int n0 = ntile * BN;
     const int V = a.V;
     // EPI_GRAPH: this tile's bias2[17][n0 .. n0 + BN) slice, loaded now so its
@@ -1093,7 +1088,10 @@ hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int 
     for (int s = 0; s <= a.nseg; ++s) {
         const XSeg& g = s < a.nseg ? a.seg[s] : a.idn;
         if (s == a.nseg && !g.src) break;
-        if (!g.src || g.cin % 32 || g.ld % 4 || g.ld < g.cin || g.rows_in * g.ld * 4 >= (1LL << 31)) return hipErrorInvalidValue;
+        // the K cursors pack cin/32 and kt into 8 bits each
+        if (!g.src || g.cin % 32 || g.cin / 32 > 255 || g.kt < 1 || g.kt > 255 || g.ld % 4 || g.ld < g.cin ||
+            g.rows_in * g.ld * 4 >= (1LL << 31))
+            return hipErrorInvalidValue;
     }
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
@@ -1131,7 +1129,10 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     for (int s = 0; s <= a.nseg; ++s) {
         const XSeg& g = s < a.nseg ? a.seg[s] : a.idn;
         if (s == a.nseg && !g.src) break;
-        if (!g.src || g.cin % 32 || g.ld % 4 || g.ld < g.cin || g.rows_in * g.ld * 4 >= (1LL << 31)) return hipErrorInvalidValue;
+        // the K cursors pack cin/32 and kt into 8 bits each
+        if (!g.src || g.cin % 32 || g.cin / 32 > 255 || g.kt < 1 || g.kt > 255 || g.ld % 4 || g.ld < g.cin ||
+            g.rows_in * g.ld * 4 >= (1LL << 31))
+            return hipErrorInvalidValue;
     }
     if (epi == EPI_GRAPH && (a.V != 17 || a.M % 17 || !a.amix || !a.bias || a.idn.src)) return hipErrorInvalidValue;
     if (a.rx && (bn != 64 || epi != EPI_BIAS || a.rxc < 0 || a.rxc > 4)) return hipErrorInvalidValue;

@@ -33,17 +33,30 @@ NUM_EXPR = 10
 
 def constants_from_npz(path: str, num_betas: int = NUM_BETAS, num_expr: int = NUM_EXPR,
                        flat_hand_mean: bool = False) -> Dict[str, np.ndarray]:
-    """SMPL-X model file -> the tensor set tik_fk_create takes (smplx
-    body_models.SMPLX.__init__ conventions: shapedirs[..., :num_betas],
-    exprdirs = shapedirs[..., 300:300+num_expr], posedirs (V,3,486) -> (486,3V),
-    parents = kintree_table[0], hand mean pose when flat_hand_mean=False)."""
+    """SMPL-X model file -> the tensor set tik_fk_create takes (public smplx
+    body_models SMPL/SMPLX.__init__ conventions, the loader smpl_util.py:13-18
+    drives through smplx.create): posedirs (V,3,486) -> (486,3V), parents =
+    kintree_table[0], hand mean pose when flat_hand_mean=False, and the shape
+    and expression bases by the file's component count —
+      * >= 400 components (SMPL-X v1.1: 300 shape + 100 expression):
+        shapedirs[..., :min(num_betas, 300)], exprdirs = shapedirs[..., 300:300+min(num_expr, 100)];
+      * fewer (the 20-component layout: 10 shape + 10 expression):
+        shapedirs[..., :min(num_betas, 10)], exprdirs = shapedirs[..., 10:10+min(num_expr, 10)]."""
     d = np.load(path, allow_pickle=False)
     sd = d["shapedirs"]
     V = d["v_template"].shape[0]
+    if sd.ndim != 3 or sd.shape[:2] != (V, 3):
+        raise ValueError(f"shapedirs must be (V, 3, components), got {sd.shape}")
+    if sd.shape[-1] < 400:   # 10 shape + 10 expression components (smplx: SHAPE_SPACE_DIM + EXPRESSION_SPACE_DIM)
+        nb, e0, ne = min(num_betas, 10), 10, min(num_expr, 10)
+    else:
+        nb, e0, ne = min(num_betas, 300), 300, min(num_expr, 100)
+    if sd.shape[-1] < e0 + ne:
+        raise ValueError(f"shapedirs has {sd.shape[-1]} components: no expression basis at [{e0}, {e0 + ne})")
     c = {
         "v_template": d["v_template"].astype(np.float32),
-        "shapedirs": sd[:, :, :num_betas].astype(np.float32),
-        "exprdirs": sd[:, :, 300:300 + num_expr].astype(np.float32),
+        "shapedirs": sd[:, :, :nb].astype(np.float32),
+        "exprdirs": sd[:, :, e0:e0 + ne].astype(np.float32),
         "posedirs": np.reshape(d["posedirs"], [-1, d["posedirs"].shape[-1]]).T.astype(np.float32),
         "J_regressor": d["J_regressor"].astype(np.float32),
         "lbs_weights": d["weights"].astype(np.float32),

@@ -114,3 +114,31 @@ def test_smplx_npz_key_mapping(tmp_path):
     np.testing.assert_array_equal(got["faces"], c["faces"])
     flat = constants_from_npz(str(path), flat_hand_mean=True)
     assert not flat["pose_mean"].any()
+
+
+def test_smplx_npz_20_component_layout(tmp_path):
+    """a model file whose shapedirs has 20 components
+    (10 shape + 10 expression, the layout public smplx reads with the
+    expression basis at [..., 10:20] when there are fewer than 400,
+    smpl_util.py:13-18 -> smplx.create) loads its expression basis from
+    columns 10:20, not from the empty 300:310; a file with too few components
+    for either basis is refused."""
+    import test_gpu_fk as fkt
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.smplx_fk import constants_from_npz
+    c = syn.synthetic_smplx_constants(seed=6, num_verts=500, num_faces=800)
+    c["extra_verts"] = np.minimum(syn.SMPLX_EXTRA_VERTS, 499).astype(np.int32)
+    path = tmp_path / "SMPLX_NEUTRAL.npz"
+    fkt._write_smplx_npz(path, c, components=20)
+    got = constants_from_npz(str(path))
+    assert got["shapedirs"].shape == (500, 3, 10) and got["exprdirs"].shape == (500, 3, 10)
+    np.testing.assert_array_equal(got["shapedirs"], c["shapedirs"])
+    np.testing.assert_array_equal(got["exprdirs"], c["exprdirs"])
+    few = constants_from_npz(str(path), num_betas=16, num_expr=16)   # clamped to 10 + 10, as smplx
+    np.testing.assert_array_equal(few["exprdirs"], c["exprdirs"])
+    d = dict(np.load(path))
+    d["shapedirs"] = d["shapedirs"][:, :, :15]
+    bad = tmp_path / "SMPLX_BAD.npz"
+    np.savez(bad, **d)
+    with pytest.raises(ValueError):
+        constants_from_npz(str(bad))

@@ -6,16 +6,17 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import f16x3_only, golden, prec_params
 from oracle import stgcn as orc
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xpt", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1", "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
-                                                 "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
-                                                 "f16x3-dmahead"])
+@pytest.fixture(scope="module", params=prec_params("bf16x3", "bf16x3-xpt", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1",
+                                                   "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
+                                                   "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
+                                                   "f16x3-dmahead"))
 def model(request):
     """bf16x3 (the default: 6-product bf16 split, fp32 range); fp32 MFMA;
     f16x3 with the default GEMM path (split-block activations with
@@ -117,7 +118,7 @@ def test_run_inference_sample(model):
     assert np.abs(y9 - r["win9"]).max() < TOL
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "fp32", "f16x3"])
+@pytest.mark.parametrize("prec", prec_params("bf16x3", "fp32", "f16x3"))
 def test_blocks_vs_golden(prec):
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.models import StGcnBlock
@@ -179,12 +180,13 @@ def test_cpu_tensor_refused(model):
         model(torch.zeros(1, 9, 17, 3))
 
 
+@f16x3_only
 def test_model_dma_subbatches_past_2gib(model):
     """4000 x 64-frame windows: the largest split-block tensor of one call
     would pass 2 GiB (32-bit buffer offsets), so the DMA path runs two
     sub-batches; windows on both sides of the split equal their solo solves."""
     if model.regressor.tik_precision != "f16x3":
-        pytest.skip("the sub-batch split belongs to the f16x3 DMA path")
+        pytest.skip("the split-block sub-batch split belongs to the f16x3 DMA path")
     from temporal_inverse_kinematics_amd import synthetic as syn
     N = 4000
     x = torch.from_numpy(syn.synthetic_windows(N, 64, seed=5)).cuda()
@@ -196,7 +198,7 @@ def test_model_dma_subbatches_past_2gib(model):
     assert (y[pick] - solo).abs().max().item() < 2e-5
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "f16x3"])
+@pytest.mark.parametrize("prec", prec_params("bf16x3", "f16x3"))
 def test_concurrent_streams_bitwise(prec):
     """Four model handles on four HIP streams running concurrently give the
     same poses, bit for bit, as the serial runs (regression: layer 0's graph
@@ -227,6 +229,7 @@ def test_concurrent_streams_bitwise(prec):
                 assert torch.equal(outs[i], ref[i])
 
 
+@f16x3_only
 def test_fused_gcn_epilogue_bitwise():
     """The next block's gcn fused into the temporal-conv epilogue
     (TG_128x128_G7) uses the separate G kernel's products and K order: the
@@ -248,15 +251,14 @@ def test_fused_gcn_epilogue_bitwise():
             assert torch.equal(fused(x)["poses"], plain(x)["poses"]), (n, T)
 
 
-@pytest.mark.parametrize("precision,lag", [("f16x3", None), ("bf16x3", None), ("bf16x3", 1), ("bf16x3", 4)])
-def test_two_stream_split_bitwise(precision, lag):
-    """Large batches run as two parts on two HIP streams (second workspace,
+@pytest.mark.parametrize("precision,nsplit", [pytest.param("f16x3", 2, marks=f16x3_only), ("bf16x3", 2), ("bf16x3", 3)])
+def test_two_stream_split_bitwise(precision, nsplit):
+    """Large batches run as parts on several HIP streams (a workspace per part,
     fork/join events): poses bit-identical to the one-stream run, including
-    an odd batch and one the DMA sub-batching also splits. bf16x3 (xgemm
-    path): also with part 1 starting after part 0's first / fourth launch
-    (TIK_SPLIT_LAG), so the parts' graph and temporal launches interleave."""
+    an odd batch and one the DMA sub-batching also splits; bf16x3 also in
+    three parts (TIK_SPLIT_N=3)."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    split = _model_with_env(precision, **({"TIK_SPLIT_LAG": lag} if lag else {}))
+    split = _model_with_env(precision, TIK_SPLIT_N=nsplit)
     one = _model_with_env(precision, TIK_SPLIT=0)
     for n in (1024, 1001, 513):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 1)).cuda()
@@ -283,22 +285,23 @@ def _model_with_env(precision="f16x3", **env):
     return m
 
 
-def test_two_stream_split_with_dma_chunks_bitwise():
+@pytest.mark.parametrize("precision", prec_params("bf16x3", "f16x3"))
+def test_two_stream_split_with_dma_chunks_bitwise(precision):
     """the split interacts with the DMA sub-batching. With
     TIK_DMA_CHUNK=600 a 1001-window batch runs as a split chunk (600 windows,
     two halves) and an unsplit tail chunk (401 windows, below the 32768-frame
     threshold); a 1500-window batch as two split chunks and a 300-window tail.
     Poses are bit-identical to one unchunked stream."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    chunked = _model_with_env(TIK_DMA_CHUNK=600)
-    one = _model_with_env(TIK_SPLIT=0)
+    chunked = _model_with_env(precision, TIK_DMA_CHUNK=600)
+    one = _model_with_env(precision, TIK_SPLIT=0)
     for n in (1001, 1500):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 7)).cuda()
         with torch.no_grad():
             assert torch.equal(chunked(x)["poses"], one(x)["poses"]), n
 
 
-@pytest.mark.parametrize("precision", ["f16x3", "bf16x3"])
+@pytest.mark.parametrize("precision", prec_params("f16x3", "bf16x3"))
 def test_two_stream_split_repeated_bitwise(precision):
     """the default two-stream split path, repeated 40
     times back to back (the halves overlap differently on every run), stays
@@ -317,14 +320,14 @@ def test_two_stream_split_repeated_bitwise(precision):
 
 def test_concurrent_streams_layer0_gcn_bitwise():
     """The kernel that once failed under concurrency (gcn0: layer 0's data_bn +
-    3->64 conv + graph mix from the raw keypoints, on the layered path that
-    TIK_STBLOCK=0 selects) runs on four HIP streams at once, beside itself:
+    3->64 conv + graph mix from the raw keypoints; on the bf16x3 path every
+    forward runs it) runs on four HIP streams at once, beside itself:
     bit-identical to serial runs."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     S = 4
     x = torch.from_numpy(syn.synthetic_windows(1024, 64, seed=5)).cuda()
     parts = list(x.chunk(S))
-    models = [_model_with_env(TIK_STBLOCK=0, TIK_SPLIT=0) for _ in range(S)]
+    models = [_model_with_env("bf16x3", TIK_SPLIT=0) for _ in range(S)]
     with torch.no_grad():
         ref = [models[i](parts[i])["poses"].clone() for i in range(S)]
         torch.cuda.synchronize()
@@ -344,6 +347,7 @@ def test_concurrent_streams_layer0_gcn_bitwise():
                 assert torch.equal(outs[i], ref[i])
 
 
+@f16x3_only
 def test_weight_stationary_tgw_bitwise():
     """The stride-1 fused blocks (L3, L4) on the weight-stationary persistent
     kernel (tgw.hip, TW_128) give poses bit-identical to the TG3 tiles
@@ -364,6 +368,7 @@ def test_weight_stationary_tgw_bitwise():
 
 
 
+@f16x3_only
 def test_persistent_gcn_gpw_bitwise():
     """The unfused gcn launches (L2 64->128, L6 128->256, L7 256->256) on the
     weight-stationary persistent kernel (gpw.hip, GP_*) give poses
@@ -521,3 +526,29 @@ def test_xgemm_persistent_layer0_close():
     with torch.no_grad():
         d = float((pt(x)["poses"] - one(x)["poses"]).abs().max())
     assert d < 1e-5, d
+
+
+@pytest.mark.parametrize("N", [4000, 8192])
+def test_bf16x3_past_2gib_and_config3_batch(N):
+    """VERDICT r3 item 3, on the default arithmetic: at T=64 one xgemm call
+    holds at most 3853 windows (every fp32 activation tensor a DMA reads stays
+    below 2 GiB: 32-bit buffer offsets; L2's z is 557,056 B per window), so
+    4000 windows run as two chunks and BASELINE config #3's 8192-window global
+    batch (inference.py:43-54 scaled) as three, on one GPU. Windows on both
+    sides of each chunk boundary equal their solo solves bit for bit (the
+    bf16x3 path is batch-invariant), sampled windows match the oracle, and
+    every pose is finite."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    m = synthetic_model(win_size=64, device="cuda", precision="bf16x3").regressor
+    x = syn.synthetic_windows(N, 64, seed=N)
+    xd = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        y = m(xd)["poses"]
+        pick = [0, 3852, 3853, 3854, 3855, N - 1] + ([7705, 7706, 7707] if N > 7706 else [])
+        solo = torch.cat([m(xd[i:i + 1])["poses"] for i in pick])
+    assert torch.isfinite(y).all()
+    assert torch.equal(y[pick], solo)
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    ref = orc.pose_regressor(x[pick[:4]], sd)["poses"]
+    assert np.abs(y[pick[:4]].cpu().numpy() - ref).max() < TOL

@@ -164,30 +164,43 @@ def load_smplx_models(smplx_dir, device, batch_size):
 
 def run_smpl_inference(data, smplx_models, device, apply_trans=True, apply_root_rot=True, apply_shape=True,
                        return_mesh=False):
-    """smpl_util.py:22-82: poses (F,>=66) [+ trans, betas] -> joints (F,144,3) [, verts (F,V,3)].
+    """smpl_util.py:22-82: poses (F,>=66) [+ trans, betas] -> joints (F,144,3) [, verts].
 
     All F frames go through one call (no fixed-size zero-padded chunks);
-    pose columns past the array's width are treated as zero."""
+    pose columns past the array's width are treated as zero. The joints come
+    back un-padded (smpl_util.py:72-74). The meshes keep the reference's
+    padding: it appends every chunk's body.vertices without the [:org_bsize]
+    slice (smpl_util.py:76-77), so it returns ceil(F / batch_size) *
+    batch_size meshes, the extra ones the bodies of all-zero inputs; here
+    those rows are solved from zero inputs too. Pinned by
+    tests/test_smpl_orchestration.py against the reference's own function."""
     model = smplx_models[str(data["gender"])]
     poses = np.asarray(data["poses"], dtype=np.float32)
     F = poses.shape[0]
+    bs = max(1, int(getattr(model, "batch_size", 1) or 1))
+    R = F + ((-F) % bs if return_mesh else 0)   # rows solved: + the reference's mesh padding
     if poses.shape[1] < 156:
         poses = np.concatenate([poses, np.zeros((F, 156 - poses.shape[1]), np.float32)], 1)
-    P = torch.from_numpy(np.ascontiguousarray(poses[:, :156])).to(device)
-    full = torch.zeros((F, 55, 3), device=device)
+    P = torch.zeros((R, 156), device=device)
+    P[:F] = torch.from_numpy(np.ascontiguousarray(poses[:, :156])).to(device)
+    full = torch.zeros((R, 55, 3), device=device)
     if apply_root_rot:
         full[:, 0] = P[:, :3]
-    full[:, 1:22] = P[:, 3:66].reshape(F, 21, 3)
-    full[:, 25:40] = P[:, 66:111].reshape(F, 15, 3)
-    full[:, 40:55] = P[:, 111:156].reshape(F, 15, 3)
-    trans = torch.from_numpy(np.asarray(data["trans"], np.float32)).to(device) if apply_trans else None
+    full[:, 1:22] = P[:, 3:66].reshape(R, 21, 3)
+    full[:, 25:40] = P[:, 66:111].reshape(R, 15, 3)
+    full[:, 40:55] = P[:, 111:156].reshape(R, 15, 3)
+    trans = None
+    if apply_trans:
+        trans = torch.zeros((R, 3), device=device)
+        trans[:F] = torch.from_numpy(np.asarray(data["trans"], np.float32)).to(device)
     betas = None
     if apply_shape:
         b = np.asarray(data["betas"], np.float32)[:model.num_betas][None]
-        betas = torch.from_numpy(np.tile(b, (F, 1))).to(device)
+        betas = torch.zeros((R, b.shape[1]), device=device)
+        betas[:F] = torch.from_numpy(np.tile(b, (F, 1))).to(device)
     with torch.no_grad():
         joints, verts = model.full_forward(full, betas, None, trans, return_verts=return_mesh)
-    j = joints.cpu().numpy()
+    j = joints[:F].cpu().numpy()
     if return_mesh:
         return j, verts.cpu().numpy()
     return j

@@ -136,3 +136,26 @@ def test_counted_wait_kernels_do_not_spill(tmp_path, src_name):
     assert not re.search(r"^\s+scratch_", text, re.M), "scratch instructions"
     spills = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", text)]
     assert spills and max(spills) == 0, spills
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["xgemm.hip", "layer0.hip", "fk.hip", "online.hip", "misc.hip"])
+def test_no_lgkmcnt_partial_wait_with_smem_outstanding(src, tmp_path):
+    """VERDICT r3 item 7 (the round-1 gcn0 corruption): SMEM
+    loads return out of order, so an `s_waitcnt lgkmcnt(N>0)` meant to retire
+    an LDS read is only valid when no s_load / s_buffer_load is in flight.
+    scripts/isa_lgkm_scan.py follows every path of each default-path kernel
+    (a dataflow over basic blocks) and finds no such wait. (It found none in
+    the pre-fix gcn0 of 283cbfa either: that hypothesis is excluded.)"""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    import isa_lgkm_scan
+    out = tmp_path / (src + ".s")
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{os.path.join(REPO, 'include')}",
+                        "--cuda-device-only", "-S", os.path.join(REPO, "temporal_inverse_kinematics_amd", "csrc", src),
+                        "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    res = isa_lgkm_scan.scan_file(str(out))
+    assert res, "no kernels found"
+    bad = {k: v[1][:3] for k, v in res.items() if v[1]}
+    assert not bad, bad

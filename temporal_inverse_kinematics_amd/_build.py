@@ -34,15 +34,18 @@ def _needs_rebuild(objs_srcs, lib):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, debug: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, debug: bool = False, verbose: bool = False, out: str = None, flags=None) -> str:
+    """Build libtik.so in-tree (or a diagnostic variant: `out` = another path,
+    `flags` = extra hipcc flags such as -DTIK_XTUNE; loaded with TIK_LIB=out)."""
     srcs = _sources()
-    objdir = os.path.join(PKG, "build")
+    lib = out or LIB
+    objdir = os.path.join(PKG, "build") if out is None else out + ".objs"
     os.makedirs(objdir, exist_ok=True)
-    if not force and not _needs_rebuild(srcs, LIB):
+    if not force and out is None and not _needs_rebuild(srcs, LIB):
         return LIB
     opt = ["-O0", "-g"] if debug else ["-O3"]
     # diagnostic builds: e.g. TIK_HIPCC_FLAGS="-DTIK_XTRACE" (xgemm phase stamps), "-DTIK_XTUNE"
-    opt += os.environ.get("TIK_HIPCC_FLAGS", "").split()
+    opt += os.environ.get("TIK_HIPCC_FLAGS", "").split() + list(flags or [])
     common = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
               f"-I{os.path.join(REPO, 'include')}", *opt]
 
@@ -60,14 +63,17 @@ def build(force: bool = False, debug: bool = False, verbose: bool = False) -> st
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
                        capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, debug="--debug" in sys.argv, verbose=True))
+    # python -m temporal_inverse_kinematics_amd._build [--debug] [--out PATH -DFLAG ...]
+    out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
+    fl = [a for a in sys.argv[1:] if a.startswith("-D")]
+    print(build(force=True, debug="--debug" in sys.argv, verbose=True, out=out, flags=fl))

@@ -67,6 +67,8 @@ def kernel_symbol(label, precision):
         # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), waves per workgroup (TIK_XNW)>
         nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
         return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
+    if label in ("XB0", "XB1"):
+        return f"tik::xblock_kernel<{'true' if label == 'XB0' else 'false'}>"
     if label == "XW128":
         return "tik::xgemm_ws_kernel"   # <identity residual>: the label does not say which (any instantiation)
     if label[:2] == "XP" and label[2:] in ("64", "128"):

@@ -27,6 +27,7 @@
 #include "misc.h"
 #include "online.h"
 #include "common.h"
+#include "xblock.h"
 #include "xgemm.h"
 
 namespace tik_host {
@@ -198,6 +199,7 @@ struct Layer {
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
+    DevHBuf xbg, xbt;       // whole-block kernel (xblock.hip, 64 channels, stride 1): gcn / tcn planes in the MFMA register layout
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
@@ -282,6 +284,10 @@ struct Layer {
                 const int ns = (res == RES_CONV && cin % 32 == 0) ? 2 : 1;
                 if ((rc = xt.upload(tik::xgemm_pack(t, ns, cout, bn)))) return rc;
                 xt_bn = bn; xt_ks = TK * cout / 32 + (ns == 2 ? cin / 32 : 0);
+            }
+            if (cout == 64 && stride == 1 && V == 17) {   // xblock.hip
+                if ((rc = xbt.upload(tik::xblock_pack_weights(hwt.data(), cout, TK * cout, TK, cout)))) return rc;
+                if (cin == 64 && (rc = xbg.upload(tik::xblock_pack_weights(hwg.data(), cout, cinp, 1, cin)))) return rc;
             }
         }
         std::vector<float> ha(A_eff.begin(), A_eff.end());
@@ -760,6 +766,8 @@ struct tik_model {
     bool tgw = true;                   // stride-1 fused blocks on the weight-stationary kernel (TIK_TGW=0: TG3)
     bool gpw = true;                   // unfused gcn launches on the persistent kernel (TIK_GPW=0: G3_272x128)
     bool xgemm = true;                 // bf16x3 backbone on xgemm.hip (TIK_XGEMM=0: register-staged cgemm.hip)
+    bool xblk = true;                  // blocks 0 and 1 as whole-block kernels (xblock.hip; TIK_XBLK=0: layered G + T)
+    int ncu = 256;                     // compute units (persistent grids)
     DevHBuf trash;                     // scratch line for the tgw kernel's stores of invalid rows
     Profiler prof;
     bool profiling = false;
@@ -785,14 +793,17 @@ static void apply_env(tik_model* md) {
     if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
     if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
     if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
+    if (const char* e = getenv("TIK_XBLK")) md->xblk = e[0] != '0';
     if (const char* e = getenv("TIK_XNW"))
         for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("TIK_XEPI"))
         for (auto& L : md->layers) L.xepi = atoi(e);
     {
         int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
             for (auto& L : md->layers) L.ncu = ncu;
+            md->ncu = ncu;
+        }
         const char* e = getenv("TIK_XPT");
         for (auto& L : md->layers) {
             // default: the 64-column temporal convs (6 K steps per tile: the
@@ -1111,13 +1122,57 @@ static int x_chunk(const tik_model* m, int T) {
 
 // Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
 // from the raw keypoints (data_bn folded into its gcn kernel).
+static bool use_xblk(const tik_model* m) {
+    if (!m->xblk || m->layers.size() < 2 || m->C0 > 4) return false;
+    const Layer& L0 = m->layers[0];
+    const Layer& L1 = m->layers[1];
+    return L0.cout == 64 && L0.stride == 1 && L0.res == RES_CONV && L0.cin == m->C0 && L0.wr0.p && L0.xbt.p &&
+           L1.cin == 64 && L1.cout == 64 && L1.stride == 1 && L1.res == RES_IDEN && L1.xbt.p && L1.xbg.p && m->V == 17;
+}
+
+// Blocks 0 and 1 as whole-block kernels (xblock.hip): block 0 from the raw
+// keypoints writes its output as bf16x3 planes into the z workspace, block 1
+// reads them and writes fp32 rows to `out`.
+static int blocks01_x(tik_model_t m, const float* x, int N, int T, float* out, hipStream_t st, const WsPtrs& w) {
+    const Layer& L0 = m->layers[0];
+    const Layer& L1 = m->layers[1];
+    const double px = (double)N * T * m->V;
+    unsigned short* p3 = reinterpret_cast<unsigned short*>(w.z);
+    tik::XBlkArgs b{};
+    b.nframes = N * T; b.T = T;
+    b.xraw = x; b.c0 = m->C0; b.bn_sc = m->bn_sc.p; b.bn_sh = m->bn_sh.p; b.wg0 = L0.wg.p; b.ldwg0 = L0.cinp; b.rw = L0.wr0.p;
+    b.wtp = L0.xbt.p; b.bias2 = L0.bias2.p; b.amix = L0.amix.p; b.mix_sparse = L0.mix_sparse ? 1 : 0; b.bias = L0.biasT.p;
+    b.out_p3 = p3; b.trash = L0.xtrash;
+    {
+        ProfScope p("XB0.L0", 2.0 * px * (L0.cin * 64 + 17 * 64) + 2.0 * px * (TK * 64 * 64 + L0.cin * 64), px * (4.0 * m->C0 + 384.0), st);
+        p.out(p3, (size_t)px * 384);
+        HIP_TRY(tik::launch_xblock(b, true, m->ncu, st));
+    }
+    tik::XBlkArgs c{};
+    c.nframes = N * T; c.T = T; c.xp3 = p3;
+    c.wgp = L1.xbg.p; c.wtp = L1.xbt.p; c.bias2 = L1.bias2.p; c.amix = L1.amix.p; c.mix_sparse = L1.mix_sparse ? 1 : 0;
+    c.bias = L1.biasT.p; c.out_f = out; c.trash = L1.xtrash;
+    {
+        ProfScope p("XB1.L1", 2.0 * px * (64 * 64 + 17 * 64) + 2.0 * px * TK * 64 * 64, px * (384.0 + 256.0), st);
+        p.out(out, (size_t)px * 256);
+        HIP_TRY(tik::launch_xblock(c, false, m->ncu, st));
+    }
+    return TIK_OK;
+}
+
 static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_out, int* tout, hipStream_t st,
                       const WsPtrs& w) {
     const float* cur = nullptr;
     int ld = 0, t = T, rc;
     float* bufs[2] = {w.a0, w.a1};
     int which = 0;
+    const bool xblk = use_xblk(m);
+    if (xblk) {
+        if ((rc = blocks01_x(m, x, N, T, w.a1, st, w))) return rc;
+        cur = w.a1; ld = 64;
+    }
     for (const Layer& L : m->layers) {
+        if (xblk && L.index < 2) continue;
         float* o = bufs[which];
         if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb);
         else rc = L.forward_x(cur, ld, N, t, w.z, o, st);

@@ -571,3 +571,28 @@ def test_xgemm_ws_bitwise(n, T):
         b = one(x)["poses"]
     assert torch.isfinite(a).all()
     assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (2, 9), (1, 1), (5, 31)])
+def test_xblock_whole_blocks_vs_layered(n, T):
+    """Blocks 0 and 1 as whole-block kernels (xblock.hip: z kept in LDS, block
+    0's output as bf16x3 planes, weights in registers; the default) against the
+    layered G + T launches (TIK_XBLK=0) and the oracle: the same bf16x3
+    products in the same K order, so the poses agree to fp32 rounding (the
+    3 -> 64 residual conv of block 0 is contracted differently), at the bench
+    size, with partial last tiles, windows shorter than a tile, single frames
+    and T=65; every pose finite."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    xb = _model_with_env("bf16x3", TIK_SPLIT=0)
+    lay = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XBLK=0)
+    x = syn.synthetic_windows(n, T, seed=n * 7 + T)
+    xd = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        a = xb(xd)["poses"].clone()
+        b = lay(xd)["poses"]
+    assert torch.isfinite(a).all()
+    assert float((a - b).abs().max()) < 2e-5, float((a - b).abs().max())
+    sd = {k: v.detach().cpu().numpy() for k, v in xb.state_dict().items()}
+    pick = list(range(min(n, 3)))
+    ref = orc.pose_regressor(x[pick], sd)["poses"]
+    assert np.abs(a.cpu().numpy()[pick] - ref).max() < TOL

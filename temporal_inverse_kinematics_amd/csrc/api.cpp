@@ -1122,6 +1122,34 @@ static int x_chunk(const tik_model* m, int T) {
 
 // Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
 // from the raw keypoints (data_bn folded into its gcn kernel).
+// debug (TIK_X_TRACE=1 with a -DTIK_XTRACE build): per-phase sums of the whole-block kernels
+static hipError_t launch_xblock_traced(tik::XBlkArgs a, bool raw, int ncu, hipStream_t st, const char* label) {
+    static const bool on = getenv("TIK_X_TRACE") != nullptr;
+    if (!on) return tik::launch_xblock(a, raw, ncu, st);
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc(&d, (size_t)ncu * 16 * 8);
+    if (e != hipSuccess) return e;
+    (void)hipMemset(d, 0, (size_t)ncu * 16 * 8);
+    a.trace = d;
+    e = tik::launch_xblock(a, raw, ncu, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<unsigned long long> h((size_t)ncu * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    double s0[6] = {0}, s4[6] = {0}, nt = 0, n = 0;
+    for (int w = 0; w < ncu; ++w) {
+        if (!h[16 * w + 7]) continue;
+        n += 1; nt += (double)h[16 * w + 6];
+        for (int k = 0; k < 6; ++k) { s0[k] += (double)h[16 * w + k]; s4[k] += (double)h[16 * w + 8 + k]; }
+    }
+    nt = std::max(1.0, nt);
+    fprintf(stderr, "XBTRACE %-8s tiles %6.0f | per tile, wave0: start %6.0f G+mix %6.0f zbar %6.0f res+dma %6.0f T %6.0f endbar %6.0f"
+            " | wave4: start %6.0f G+mix %6.0f zbar %6.0f res+dma %6.0f T %6.0f endbar %6.0f\n", label, nt,
+            s0[0] / nt, s0[1] / nt, s0[2] / nt, s0[3] / nt, s0[4] / nt, s0[5] / nt, s4[0] / nt, s4[1] / nt, s4[2] / nt,
+            s4[3] / nt, s4[4] / nt, s4[5] / nt);
+    return e;
+}
+
 static bool use_xblk(const tik_model* m) {
     if (!m->xblk || m->layers.size() < 2 || m->C0 > 4) return false;
     const Layer& L0 = m->layers[0];
@@ -1146,7 +1174,7 @@ static int blocks01_x(tik_model_t m, const float* x, int N, int T, float* out, h
     {
         ProfScope p("XB0.L0", 2.0 * px * (L0.cin * 64 + 17 * 64) + 2.0 * px * (TK * 64 * 64 + L0.cin * 64), px * (4.0 * m->C0 + 384.0), st);
         p.out(p3, (size_t)px * 384);
-        HIP_TRY(tik::launch_xblock(b, true, m->ncu, st));
+        HIP_TRY(launch_xblock_traced(b, true, m->ncu, st, "XB0.L0"));
     }
     tik::XBlkArgs c{};
     c.nframes = N * T; c.T = T; c.xp3 = p3;
@@ -1155,7 +1183,7 @@ static int blocks01_x(tik_model_t m, const float* x, int N, int T, float* out, h
     {
         ProfScope p("XB1.L1", 2.0 * px * (64 * 64 + 17 * 64) + 2.0 * px * TK * 64 * 64, px * (384.0 + 256.0), st);
         p.out(out, (size_t)px * 256);
-        HIP_TRY(tik::launch_xblock(c, false, m->ncu, st));
+        HIP_TRY(launch_xblock_traced(c, false, m->ncu, st, "XB1.L1"));
     }
     return TIK_OK;
 }

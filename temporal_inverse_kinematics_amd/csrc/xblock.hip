@@ -172,8 +172,22 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
     const int blk0 = ph * NB;
     const int nblk = ph == 0 ? NB : TBLK - NB;
 
+#ifdef TIK_XTRACE
+    const bool tr = a.trace != nullptr && (wave == 0 || wave == 4);
+#else
+    constexpr bool tr = false;
+#endif
+    unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (i >= 0) ph_[i] += t - tlast;
+            tlast = t;
+        }
+    };
     for (int tile = t_begin; tile < t_end; ++tile) {
         const int q0 = tile * F;
+        stamp(-1);
         asm volatile("" : "+v"(tid), "+v"(lane));
         g = lane >> 4;
         cho = 16 * cg + 4 * g;
@@ -187,6 +201,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 if (i < FIN * V * 4) kps[i] = kok[jj] ? fmaf(kx[jj], ksc[jj], ksh[jj]) : 0.f;
             }
             __syncthreads();
+            stamp(0);
             if (tile + 1 < t_end) load_kp(tile + 1);   // lands under this tile's work
             // thread (frame f, channel quad c4) of a joint half: waves 0-3 joints 0-8,
             // waves 4-7 joints 9-16 (gcn0_kernel's arithmetic, layer0.hip)
@@ -245,6 +260,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             // x image landed (every wave waits for its own DMA share, then the barrier)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            stamp(0);
             if (wave >= 4) load_wt();
             if (wave < 4) {
                 // G transposed: y^T = Wg' x^T; pixel block j = joint j of the tile's frames
@@ -306,7 +322,9 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 }
             }
         }
+        stamp(1);
         __syncthreads();   // z image complete
+        stamp(2);
 
         // ================= 2. the residual of this wave's output pixels (before the
         // next tile's data overwrites its source), then the next tile's x image
@@ -348,6 +366,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             __syncthreads();
             if (tile + 1 < t_end) issue_x(tile + 1);
         }
+        stamp(3);
 
         // ================= 3. T: 3 taps x 2 K blocks from the z image, this wave's pixel blocks
 #pragma unroll
@@ -413,7 +432,14 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
         // every wave done reading the z image (and, block 0, the keypoint image)
         // before the next tile writes them
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stamp(4);
         __syncthreads();
+        stamp(5);
+    }
+    if (tr && lane == 0) {
+        unsigned long long* o = a.trace + 16 * (size_t)blockIdx.x + (wave == 4 ? 8 : 0);
+        for (int i = 0; i < 6; ++i) o[i] = ph_[i];
+        o[6] = t_end - t_begin; o[7] = 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

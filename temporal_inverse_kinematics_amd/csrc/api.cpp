@@ -29,6 +29,7 @@
 #include "common.h"
 #include "xblock.h"
 #include "xgemm.h"
+#include "xgraph.h"
 
 namespace tik_host {
 thread_local std::string g_err;
@@ -199,11 +200,13 @@ struct Layer {
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
+    DevHBuf xgw;            // weight-stationary gcn kernel (xgraph.hip, 128 / 256 output channels): gcn planes in the MFMA register layout
     DevHBuf xbg, xbt;       // whole-block kernel (xblock.hip, 64 channels, stride 1): gcn / tcn planes in the MFMA register layout
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
+    int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers)
     int xws = 0;            // 128-column temporal convs on the warp-specialized persistent kernel (launch_xgemm_ws; TIK_XWS bit mask of layers; off: measured 3-9 % slower)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
@@ -285,6 +288,8 @@ struct Layer {
                 if ((rc = xt.upload(tik::xgemm_pack(t, ns, cout, bn)))) return rc;
                 xt_bn = bn; xt_ks = TK * cout / 32 + (ns == 2 ? cin / 32 : 0);
             }
+            if ((cout == 128 || cout == 256) && (cin == 64 || cin == 128 || cin == 256) && V == 17)   // xgraph.hip
+                if ((rc = xgw.upload(tik::xblock_pack_weights(hwg.data(), cout, cinp, 1, cin)))) return rc;
             if (cout == 64 && stride == 1 && V == 17) {   // xblock.hip
                 if ((rc = xbt.upload(tik::xblock_pack_weights(hwt.data(), cout, TK * cout, TK, cout)))) return rc;
                 if (cin == 64 && (rc = xbg.upload(tik::xblock_pack_weights(hwg.data(), cout, cinp, 1, cin)))) return rc;
@@ -370,6 +375,16 @@ struct Layer {
             ProfScope p("G0f_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout, 4.0 * (px_in * cin + px_in * cout), st);
             HIP_TRY(tik::launch_gcn0_f32(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
                                          cout, z, cout, xb4, st));
+        } else if (xgwon && xgw.p && xtrash) {
+            tik::XGraphArgs g{};
+            g.nframes = N * tin; g.x = x; g.ldx = ld; g.cin = cin; g.cout = cout; g.wp = xgw.p;
+            g.bias2 = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout;
+            g.nts = xnts(index); g.trash = xtrash;
+            const std::string lab = "XGW.L" + std::to_string(index);
+            ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
+                        4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
+            p.out(z, (size_t)rin * cout * 4);
+            HIP_TRY(tik::launch_xgraph(g, ncu, st));
         } else {
             tik::XArgs g{};
             g.M = (int)rin; g.Nc = cout; g.V = V; g.tout = tin;
@@ -810,6 +825,7 @@ static void apply_env(tik_model* md) {
             // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
             L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
             if (const char* w = getenv("TIK_XWS")) L.xws = (atoi(w) >> L.index) & 1;
+            if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
             L.xtrash = reinterpret_cast<float*>(md->trash.p);
         }
     }

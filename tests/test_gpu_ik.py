@@ -596,3 +596,22 @@ def test_xblock_whole_blocks_vs_layered(n, T):
     pick = list(range(min(n, 3)))
     ref = orc.pose_regressor(x[pick], sd)["poses"]
     assert np.abs(a.cpu().numpy()[pick] - ref).max() < TOL
+
+
+@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (2, 9), (1, 1), (5, 31)])
+def test_xgraph_vs_tiled(n, T):
+    """The gcn of the 128 / 256-channel blocks as the weight-stationary
+    persistent kernel (xgraph.hip: weights in registers, joint-major MFMA
+    blocks, graph mix in registers; the default) against the tiled XG128 kernel
+    (TIK_XGW=0): the same bf16x3 products in the same K order and the same mix
+    order, so the poses are bit-identical — at the bench size, partial last
+    frame groups, windows shorter than a group, single frames and T=65."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    xg = _model_with_env("bf16x3", TIK_SPLIT=0)
+    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XGW=0)
+    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n * 5 + T)).cuda()
+    with torch.no_grad():
+        a = xg(x)["poses"].clone()
+        b = tl(x)["poses"]
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).abs().max())

@@ -17,6 +17,8 @@ struct XGraphArgs {
     int ldo;
     int nts;                     // nontemporal stores
     float* trash;                // >= 16 B: store target of frames past the batch
+    int tune;
+    unsigned long long* trace;   // diagnostic builds (-DTIK_XTRACE): per workgroup, waves 0 and 4, 8 counters each                    // diagnostic builds (-DTIK_XTUNE) only: bits switch parts off (1 x loads, 2 split, 4 MFMAs, 8 stores, 16 mix)
 };
 
 bool xgraph_ok(const XGraphArgs& a);

@@ -11,14 +11,17 @@
 //   * MFMA transposed with JOINT-MAJOR pixel blocks (block j = joint j of the
 //     tile's 16 frames): each lane ends with y for one frame, 4 channels and
 //     all 17 joints, so the mix + bias2 + ReLU run in registers, no C tile;
-//   * the fp32 rows of one K step (16 frames x 17 joints x 32 channels) arrive
-//     by LDS-DMA in a staging slot and are split ONCE, cooperatively, into an
+//   * the fp32 rows of one K step (16 frames x 17 joints x 32 channels: 272
+//     consecutive rows, 128 B each) are loaded into REGISTERS, D steps ahead
+//     (D = 2: two steps, ~70 KB per CU, in flight — an HBM-bound kernel needs
+//     that much to cover the loaded latency; an LDS staging slot would not
+//     fit beside the planes images), and split ONCE, cooperatively, into an
 //     LDS image of bf16 planes that all eight waves read (split on read, each
 //     wave would split every element again); the planes image is double-
-//     buffered, so step k+1's split runs beside step k's MFMAs, and the DMA of
-//     step k+2 lands during step k+1 — across tile boundaries (persistent).
+//     buffered, so step k+1's split runs beside step k's MFMAs, one barrier
+//     per step, across tile boundaries (persistent).
 // Products, K order and mix order as the tiled kernel (bf16x3 six products,
-// fp32 accumulation; bias2 then v ascending).
+// fp32 accumulation; bias2 then v ascending): bit-identical poses.
 // Tiles: (16-frame group, pass): a 256-channel output runs as two passes of
 // 128 channels (eight waves x 16). Frames are flattened over windows (a 1x1
 // conv has no temporal taps, so tiles may straddle windows).
@@ -32,30 +35,40 @@ namespace tik {
 
 namespace xg {
 constexpr int V = 17, FR = 16, PX = FR * V;          // frames per tile, pixels (272)
-constexpr int SBYTES = PX * 128;                     // fp32 staging of one K step (32 channels)
-constexpr int SINST = SBYTES / 1024;                 // 34 DMA instructions
+constexpr int NU = PX * 8;                           // 16-B units of one K step (2176)
+constexpr int NLD = (NU + 511) / 512;                // register loads per lane per step (5; the 5th on waves 0-1)
 constexpr int PROWB = 3 * 32 * 2;                    // planes image row: 3 planes x 32 channels x 2 B
 constexpr int PBYTES = PX * PROWB;                   // 52,224
-constexpr int NCHUNK = PX * 4;                       // split work items: 8-channel chunks
 }  // namespace xg
 
 // planes image: row R = 16 j + f (joint-major), unit (plane p, K group u) at
 // p * 4 + (u ^ ((R >> 1) & 3)): conflict-free b128 reads of 16 consecutive rows
 __device__ __forceinline__ int xg_unit(int R, int p, int u) { return R * xg::PROWB + ((p * 4 + (u ^ ((R >> 1) & 3))) << 4); }
 
-template <int NK>
+__device__ f32x4 tik_llvm_raw_buffer_load_v4f32(i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+
+typedef __bf16 xbf16x4 __attribute__((ext_vector_type(4)));
+
+#ifdef TIK_XTUNE
+#define XG_OFF(bit) (a.tune & (bit))
+#else
+#define XG_OFF(bit) false
+#endif
+
+template <int NK, int NP>
 __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
     using namespace xg;
+    constexpr int D = NK <= 4 ? 2 : 1;   // steps of prefetch in registers (NK = 8: the weights take 96 VGPRs)
     constexpr int B2MAX = V * 256 * 4;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[SBYTES + 2 * PBYTES + B2MAX];
-    unsigned char* const stg = smem;
-    float* const b2s = reinterpret_cast<float*>(smem + SBYTES + 2 * PBYTES);
-    auto pimg = [&](int s) __attribute__((always_inline)) { return smem + SBYTES + (s & 1) * PBYTES; };
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PBYTES + B2MAX];
+    float* const b2s = reinterpret_cast<float*>(smem + 2 * PBYTES);
+    auto pimg = [&](int s) __attribute__((always_inline)) { return smem + (s & 1) * PBYTES; };
 
     int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int QO = a.nframes, M = QO * V;
-    const int npass = a.cout / 128;
+    constexpr int npass = NP;
     const int nfg = (QO + FR - 1) / FR;
     const int ntiles = nfg * npass;
     int t_begin, t_end;
@@ -73,94 +86,112 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
     auto tile_fg = [&](int t) __attribute__((always_inline)) { return t / npass; };
     auto tile_pass = [&](int t) __attribute__((always_inline)) { return t - (t / npass) * npass; };
 
-    // bias2 [17][cout] and A_eff in VGPRs (v_readlane) before any DMA
+    // bias2 [17][cout] in LDS, A_eff in VGPRs (v_readlane)
     for (int i = tid; i < V * a.cout; i += 512) b2s[i] = a.bias2[i];
     float amv[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) amv[k] = 64 * k + lane < V * V ? a.amix[64 * k + lane] : 0.f;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
-    // ---- the fp32 rows of global step s (tile t_begin + s / NK, K block s % NK) into the staging slot
+    // ---- the fp32 rows of global step s (tile t_begin + s / NK, K block s % NK):
+    // unit U = 512 i + tid: group row m = U / 8 (frame m / 17, joint m % 17), channels 4 (U % 8) ..
     const i32x4 rX = buf_rsrc(a.x, (unsigned)((long long)M * a.ldx * 4));
-    auto issue = [&](int s) __attribute__((always_inline)) {
+    f32x4 rb[D][NLD];
+    // Every wave issues NLD loads for every step, past the batch / the run as
+    // out-of-range (zero) loads: no branch, so the compiler's vmcnt accounting
+    // stays exact (at a merge it falls back to the fewest outstanding, i.e. vmcnt(0))
+    auto load = [&](int s, f32x4 (&r)[NLD]) __attribute__((always_inline)) {
         const int t = t_begin + s / NK, kb = s - (s / NK) * NK;
         const int q0 = tile_fg(t) * FR;
+        const bool live = s < total;
 #pragma unroll
-        for (int i = 0; i < (SINST + 7) / 8; ++i) {
-            const int ins = wave + 8 * i;
-            if (ins >= SINST) break;
-            const int U = ins * 64 + lane;            // staging unit: row U / 8 (R = 16 j + f), unit U % 8
-            const int R = U >> 3, u = U & 7, j = R >> 4, f = R & 15, q = q0 + f;
-            const unsigned off = q < QO ? (unsigned)(((long long)q * V + j) * a.ldx * 4 + kb * 128 + u * 16) : DMA_OOB;
-            dma16(rX, stg + ins * 1024, off, 0);
+        for (int i = 0; i < NLD; ++i) {
+            const int U = 512 * i + tid, m = U >> 3, u = U & 7;
+            const int q = q0 + m / V;
+            const unsigned off = live && U < NU && q < QO && !XG_OFF(1) ? (unsigned)(((long long)q0 * V + m) * a.ldx * 4 + kb * 128 + u * 16) : DMA_OOB;
+            r[i] = tik_llvm_raw_buffer_load_v4f32(rX, (int)off, 0, 0);
         }
     };
-    // ---- split this wave's staging rows (the rows its own DMA instructions
-    // fill: ins = wave + 8 i) into planes image (s & 1); chunk = 8 channels of a row
-    auto split = [&](int s) __attribute__((always_inline)) {
+    // ---- split registers r (this lane's units of step s) into planes image (s & 1)
+    auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
         unsigned char* P = pimg(s);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int ins = wave + 8 * (2 * i + (lane >> 5));
-            if (ins < SINST) {
-                const int R = 8 * ins + ((lane & 31) >> 2), u = lane & 3;
-                const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + R * 128 + u * 32);
-                const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + R * 128 + u * 32 + 16);
-                xbf16x8 p0, p1, p2;
-                xsplit8(lo, hi, p0, p1, p2);
-                *reinterpret_cast<xbf16x8*>(P + xg_unit(R, 0, u)) = p0;
-                *reinterpret_cast<xbf16x8*>(P + xg_unit(R, 1, u)) = p1;
-                *reinterpret_cast<xbf16x8*>(P + xg_unit(R, 2, u)) = p2;
+        for (int i = 0; i < NLD; ++i) {
+            const int U = 512 * i + tid;
+            if (i + 1 < NLD || U < NU) {
+                const int m = U >> 3, u = U & 7;
+                const int R = 16 * (m % V) + m / V;
+                xbf16x4 p0, p1, p2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
+                    const float x = r[i][e];
+                    const __bf16 b0 = (__bf16)x;
+                    const float r1 = x - (float)b0;
+                    const __bf16 b1 = (__bf16)r1;
+                    p0[e] = b0;
+                    p1[e] = b1;
+                    p2[e] = (__bf16)(r1 - (float)b1);
+                }
+                const int h = (u & 1) * 8;
+                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 0, u >> 1) + h) = p0;
+                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 1, u >> 1) + h) = p1;
+                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 2, u >> 1) + h) = p2;
             }
         }
     };
 
-    // weights of this wave's 16 channels for the current pass (re-loaded when the pass changes)
+    // weights of this wave's 16 channels for the current pass. Two passes (256
+    // channels): K block kb's planes are re-loaded for the next tile's pass right
+    // after step kb's MFMAs, a whole tile before their next use
     xbf16x8 w[NK][3];
-    auto load_w = [&](int pass) __attribute__((always_inline)) {
+    auto load_wk = [&](int pass, int kb) __attribute__((always_inline)) {
         const int cg = pass * 8 + wave;
-        const unsigned short* wp = a.wp;
 #pragma unroll
-        for (int kb = 0; kb < NK; ++kb)
+        for (int p = 0; p < 3; ++p)
+            w[kb][p] = *reinterpret_cast<const xbf16x8*>(a.wp + ((((size_t)cg * NK + kb) * 3 + p) * 64 + lane) * 8);
+    };
+    auto load_w = [&](int pass) __attribute__((always_inline)) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
-                w[kb][p] = *reinterpret_cast<const xbf16x8*>(wp + ((((size_t)cg * NK + kb) * 3 + p) * 64 + lane) * 8);
+        for (int kb = 0; kb < NK; ++kb) load_wk(pass, kb);
     };
 
-    // prologue: weights; step 0 -> staging -> planes[0]; step 1 into the staging
-    // rows. A wave only ever reads the staging rows its own DMA fills, so the
-    // staging needs no barrier: each wave refills its rows right after its split.
+    // prologue: weights; step 0 -> planes[0]; steps 1 .. D into registers
+    load(0, rb[0]);
     load_w(tile_pass(t_begin));
-    issue(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    split(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (1 < total) issue(1);
+    split(0, rb[0]);
+#pragma unroll
+    for (int d = 1; d <= D; ++d) load(d, rb[d % D]);
 
     f32x4 acc[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // vector-memory ops this wave issued after its DMA of the next step (weight
-    // loads, epilogue stores): they may stay in flight at that DMA's wait
-    int n_after = 0;
-    auto wait_after = [&](int n) __attribute__((always_inline)) {   // n in {0, V, 3 NK, 3 NK + V}
-        if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (n == V) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-        else if (n == 3 * NK) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NK) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NK + V) : "memory");
-    };
 
-    // one K step; KB compile-time so the weights stay in registers (a runtime
-    // index into w[][] puts the array in scratch)
+#ifdef TIK_XTRACE
+    const bool tr = a.trace != nullptr && (wave == 0 || wave == 4);
+#else
+    constexpr bool tr = false;
+#endif
+    // phases: 0 barrier, 1 MFMAs j < 4, 2 split, 3 loads, 4 MFMAs j >= 4, 5 epilogue
+    unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, tlast = 0, tstart = 0;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (i >= 0) ph_[i] += t - tlast;
+            else tstart = t;
+            tlast = t;
+        }
+    };
+    stamp(-1);
+
+    // one K step; KB compile-time so the weights and the prefetch registers are
+    // statically indexed (s % D == KB % D: NK is even)
     auto step = [&](int s, int t, int pass, auto KBc) __attribute__((always_inline)) {
         constexpr int kb = decltype(KBc)::value;
+        constexpr int nb = (kb + 1) % D;   // registers holding step s+1
         asm volatile("" : "+v"(tid), "+v"(lane));   // lane-derived addresses: not hoisted across steps (spills)
         const int g = lane >> 4, f = lane & 15;
-        // every wave's split(s) landed; every wave done with step s-1's planes (the buffer split(s+1) writes).
-        // s_barrier alone: __syncthreads' release fence would wait for the DMA in flight
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        // MFMAs of step s (planes s & 1), the split of step s+1 (planes (s+1) & 1) beside them
+        // every wave's split(s) landed; every wave done with step s-1's planes (the buffer split(s+1) writes)
+        lds_barrier();
+        stamp(0);
         const unsigned char* P = pimg(s);
         xbf16x8 xb[2][3];
         auto rd = [&](int j, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
@@ -169,6 +200,7 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         };
         auto mfma_j = [&](int j) __attribute__((always_inline)) {
             if (j + 1 < V) rd(j + 1, xb[(j + 1) & 1]);
+            if (XG_OFF(4)) return;
             const xbf16x8(&x)[3] = xb[j & 1];
             // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgemm's product order
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[kb][0], x[2], acc[j], 0, 0, 0);
@@ -182,24 +214,15 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         rd(0, xb[0]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_j(j);
-        if (s + 1 < total) {
-            // this wave's rows of step s+1 landed (DMA issued one step ago): split them beside the MFMAs
-            wait_after(n_after);
-            n_after = 0;
-            split(s + 1);
-        }
+        stamp(1);
+        if (!XG_OFF(2)) split(s + 1, rb[nb]);   // VALU + LDS writes beside the MFMAs (past the run: zeros, never read)
+        stamp(2);
+        load(s + 1 + D, rb[nb]);
+        stamp(3);
 #pragma unroll
-        for (int j = 4; j < 8; ++j) mfma_j(j);
-        if (s + 2 < total) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the split's staging reads done
-            issue(s + 2);
-        }
-#pragma unroll
-        for (int j = 8; j < V; ++j) mfma_j(j);
-        if (kb == NK - 1 && s + 1 < total && tile_pass(t + 1) != pass) {
-            load_w(tile_pass(t + 1));   // the next tile's pass: behind the DMA, ahead of the stores
-            n_after += NK * 3;
-        }
+        for (int j = 4; j < V; ++j) mfma_j(j);
+        stamp(4);
+        if constexpr (NP == 2) load_wk(tile_pass(t + 1), kb);
         if constexpr (kb == NK - 1) {
             // ---- epilogue: the graph mix in registers (lane: frame f, channels co .. co + 3, all 17 joints)
             const int co = pass * 128 + 16 * wave + 4 * g;
@@ -211,7 +234,9 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
                     f32x4 z = *reinterpret_cast<const f32x4*>(b2s + wj * a.cout + co);
 #pragma unroll
                     for (int v = 0; v < V; ++v)
-                        if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
+                        if (XG_OFF(16)) {
+                            if (v == wj) z += acc[v];
+                        } else if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
                             const float av = __builtin_bit_cast(
                                 float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + wj) / 64]), (v * V + wj) % 64));
                             z += av * acc[v];
@@ -219,14 +244,14 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
                     float* o = q < QO ? a.out + ((size_t)q * V + wj) * a.ldo + co : a.trash;
-                    xst4(o, z, a.nts);
+                    if (!XG_OFF(8)) xst4(o, z, a.nts);
                 }
             };
             if (a.mix_sparse) mix_all(std::true_type{});
             else mix_all(std::false_type{});
-            n_after += V;
 #pragma unroll
             for (int j = 0; j < V; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            stamp(5);
         }
     };
     for (int t = t_begin; t < t_end; ++t) {
@@ -245,6 +270,15 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef TIK_XTRACE
+    if (tr && lane == 0) {
+        unsigned long long* o = a.trace + 16 * (size_t)blockIdx.x + (wave == 4 ? 8 : 0);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) o[i] = ph_[i];
+        o[6] = (unsigned long long)total;
+        o[7] = tlast - tstart;
+    }
+#endif
 }
 
 bool xgraph_ok(const XGraphArgs& a) {
@@ -267,9 +301,10 @@ hipError_t launch_xgraph(const XGraphArgs& a, int ncu, hipStream_t st) {
         c.out = a.out + (size_t)q0 * 17 * a.ldo;
         const int ntiles = ((c.nframes + xg::FR - 1) / xg::FR) * (a.cout / 128);
         const int grid = std::min(ntiles, ncu);
-        if (a.cin == 64) hipLaunchKernelGGL(xgraph_kernel<2>, dim3(grid), dim3(512), 0, st, c);
-        else if (a.cin == 128) hipLaunchKernelGGL(xgraph_kernel<4>, dim3(grid), dim3(512), 0, st, c);
-        else hipLaunchKernelGGL(xgraph_kernel<8>, dim3(grid), dim3(512), 0, st, c);
+        const bool two = a.cout == 256;
+        if (a.cin == 64) hipLaunchKernelGGL((two ? xgraph_kernel<2, 2> : xgraph_kernel<2, 1>), dim3(grid), dim3(512), 0, st, c);
+        else if (a.cin == 128) hipLaunchKernelGGL((two ? xgraph_kernel<4, 2> : xgraph_kernel<4, 1>), dim3(grid), dim3(512), 0, st, c);
+        else hipLaunchKernelGGL((two ? xgraph_kernel<8, 2> : xgraph_kernel<8, 1>), dim3(grid), dim3(512), 0, st, c);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -187,7 +187,32 @@ struct ProfScope {
 };
 
 // One StGcnBlock with BN folded into packed fp32 weights.
-static hipError_t launch_xgraph_traced(tik::XGraphArgs a, int ncu, hipStream_t st, const char* label);
+static hipError_t launch_xgraph_traced(tik::XGraphArgs a, int ncu, hipStream_t st, const char* label) {
+    static const bool on = getenv("TIK_X_TRACE") != nullptr;
+    if (!on) return tik::launch_xgraph(a, ncu, st);
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc(&d, (size_t)ncu * 16 * 8);
+    if (e != hipSuccess) return e;
+    (void)hipMemset(d, 0, (size_t)ncu * 16 * 8);
+    a.trace = d;
+    e = tik::launch_xgraph(a, ncu, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<unsigned long long> h((size_t)ncu * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    double s0[8] = {0}, s4[8] = {0}, n = 0;
+    for (int w = 0; w < ncu; ++w) {
+        if (!h[16 * w + 6]) continue;
+        n += 1;
+        for (int k = 0; k < 8; ++k) { s0[k] += (double)h[16 * w + k]; s4[k] += (double)h[16 * w + 8 + k]; }
+    }
+    const double ns = std::max(1.0, s0[6]);
+    fprintf(stderr, "XGTRACE %-8s wgs %4.0f steps/wg %5.1f total/wg %8.0f | per step, wave0: bar %6.0f mfma0-3 %6.0f split %6.0f load %6.0f mfma4-16 %6.0f epi %6.0f"
+            " | wave4: bar %6.0f mfma0-3 %6.0f split %6.0f load %6.0f mfma4-16 %6.0f epi %6.0f\n", label, n, s0[6] / std::max(1.0, n),
+            s0[7] / std::max(1.0, n), s0[0] / ns, s0[1] / ns, s0[2] / ns, s0[3] / ns, s0[4] / ns, s0[5] / ns, s4[0] / ns, s4[1] / ns,
+            s4[2] / ns, s4[3] / ns, s4[4] / ns, s4[5] / ns);
+    return e;
+}
 
 struct Layer {
     int cin = 0, cinp = 0, cout = 0, stride = 1, res = RES_IDEN, V = 17, index = 0;
@@ -1165,33 +1190,6 @@ static hipError_t launch_xblock_traced(tik::XBlkArgs a, bool raw, int ncu, hipSt
             " | wave4: start %6.0f G+mix %6.0f zbar %6.0f res+dma %6.0f T %6.0f endbar %6.0f\n", label, nt,
             s0[0] / nt, s0[1] / nt, s0[2] / nt, s0[3] / nt, s0[4] / nt, s0[5] / nt, s4[0] / nt, s4[1] / nt, s4[2] / nt,
             s4[3] / nt, s4[4] / nt, s4[5] / nt);
-    return e;
-}
-
-static hipError_t launch_xgraph_traced(tik::XGraphArgs a, int ncu, hipStream_t st, const char* label) {
-    static const bool on = getenv("TIK_X_TRACE") != nullptr;
-    if (!on) return tik::launch_xgraph(a, ncu, st);
-    unsigned long long* d = nullptr;
-    hipError_t e = hipMalloc(&d, (size_t)ncu * 16 * 8);
-    if (e != hipSuccess) return e;
-    (void)hipMemset(d, 0, (size_t)ncu * 16 * 8);
-    a.trace = d;
-    e = tik::launch_xgraph(a, ncu, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    std::vector<unsigned long long> h((size_t)ncu * 16);
-    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    double s0[8] = {0}, s4[8] = {0}, n = 0;
-    for (int w = 0; w < ncu; ++w) {
-        if (!h[16 * w + 6]) continue;
-        n += 1;
-        for (int k = 0; k < 8; ++k) { s0[k] += (double)h[16 * w + k]; s4[k] += (double)h[16 * w + 8 + k]; }
-    }
-    const double ns = std::max(1.0, s0[6]);
-    fprintf(stderr, "XGTRACE %-8s wgs %4.0f steps/wg %5.1f total/wg %8.0f | per step, wave0: bar %6.0f mfma0-3 %6.0f split %6.0f load %6.0f mfma4-16 %6.0f epi %6.0f"
-            " | wave4: bar %6.0f mfma0-3 %6.0f split %6.0f load %6.0f mfma4-16 %6.0f epi %6.0f\n", label, n, s0[6] / std::max(1.0, n),
-            s0[7] / std::max(1.0, n), s0[0] / ns, s0[1] / ns, s0[2] / ns, s0[3] / ns, s0[4] / ns, s0[5] / ns, s4[0] / ns, s4[1] / ns,
-            s4[2] / ns, s4[3] / ns, s4[4] / ns, s4[5] / ns);
     return e;
 }
 

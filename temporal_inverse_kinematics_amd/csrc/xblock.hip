@@ -269,18 +269,23 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
 #pragma unroll
                 for (int j = 0; j < V; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 const int fs = lane & 15, fr = fs < FIN ? fs : fs - FIN;
-                xbf16x8 xb[2][3];
-                auto rd = [&](int j, int kb, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
-                    const int R = j * FIN + fr;
+                // operand ring: step s + XPF's planes are read while step s's MFMAs run (the
+                // sched_barrier keeps the scheduler from sinking the reads next to their use)
+                constexpr int XPF = 2;
+                xbf16x8 xb[XPF + 1][3];
+                auto rd = [&](int s, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
+                    const int R = (s >> 1) * FIN + fr, kb = s & 1;
 #pragma unroll
                     for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(ximg + xb_unit(R, p, 4 * kb + g));
                 };
-                rd(0, 0, xb[0]);
+#pragma unroll
+                for (int s = 0; s < XPF; ++s) rd(s, xb[s]);
 #pragma unroll
                 for (int s = 0; s < 2 * V; ++s) {
                     const int j = s >> 1, kb = s & 1;
-                    if (s + 1 < 2 * V) rd((s + 1) >> 1, (s + 1) & 1, xb[(s + 1) & 1]);
-                    const xbf16x8(&x)[3] = xb[s & 1];
+                    if (s + XPF < 2 * V) rd(s + XPF, xb[(s + XPF) % (XPF + 1)]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const xbf16x8(&x)[3] = xb[s % (XPF + 1)];
                     // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgemm's product order
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[2], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][1], x[1], acc[j], 0, 0, 0);
@@ -288,7 +293,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[1], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][1], x[0], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[0], acc[j], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);   // one step's reads in flight at a time
+                    __builtin_amdgcn_sched_barrier(0);
                 }
                 load_wt();   // its latency hides under the mix
                 // graph mix in registers: lane = frame fs, channels cho .. cho + 3, all 17 joints
@@ -368,31 +373,38 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
         }
         stamp(3);
 
-        // ================= 3. T: 3 taps x 2 K blocks from the z image, this wave's pixel blocks
+        // ================= 3. T: 3 taps x 2 K blocks from the z image, this wave's pixel
+        // blocks, as one flattened (block, K step) loop so the operand ring runs across blocks
+        int rows[NB][3];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            if (b >= nblk) break;
             const int p = (blk0 + b) * 16 + (lane & 15);
             const int fo = p / V, jt = p - fo * V;
             const int q = q0 + fo, tw = q % T;
-            int rows[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                const bool ok = p < TPX && q < QO && tw + k - 1 >= 0 && tw + k - 1 < T;
-                rows[k] = ok ? (fo + k) * V + jt : ZR;
+                const bool ok = b < nblk && p < TPX && q < QO && tw + k - 1 >= 0 && tw + k - 1 < T;
+                rows[b][k] = ok ? (fo + k) * V + jt : ZR;
             }
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            xbf16x8 zb[2][3];
-            auto rdz = [&](int s, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
-                const int k = s >> 1, kb = s & 1;
+        }
+        {
+            constexpr int ZPF = 2, NS = 6 * NB;
+            xbf16x8 zb[ZPF + 1][3];
+            auto rdz = [&](int i, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
+                const int b = i / 6, s = i % 6, k = s >> 1, kb = s & 1;
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) d[pl] = *reinterpret_cast<const xbf16x8*>(zimg + xb_unit(rows[k], pl, 4 * kb + g));
+                for (int pl = 0; pl < 3; ++pl) d[pl] = *reinterpret_cast<const xbf16x8*>(zimg + xb_unit(rows[b][k], pl, 4 * kb + g));
             };
-            rdz(0, zb[0]);
 #pragma unroll
-            for (int s = 0; s < 6; ++s) {   // K step s = (tap s / 2, K block s % 2): xgemm's K order
-                if (s + 1 < 6) rdz(s + 1, zb[(s + 1) & 1]);
-                const xbf16x8(&z)[3] = zb[s & 1];
+            for (int i = 0; i < ZPF; ++i) rdz(i, zb[i]);
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {   // K step s = (tap s / 2, K block s % 2): xgemm's K order
+                const int b = i / 6, s = i % 6;
+                if (b >= nblk) break;
+                if (i + ZPF < NS) rdz(i + ZPF, zb[(i + ZPF) % (ZPF + 1)]);
+                __builtin_amdgcn_sched_barrier(0);
+                const xbf16x8(&z)[3] = zb[i % (ZPF + 1)];
                 const xbf16x8(&w)[3] = wt[s >> 1][s & 1];
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], z[2], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], z[1], acc, 0, 0, 0);
@@ -401,32 +413,37 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], z[0], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], z[0], acc, 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
-            }
-            // epilogue: lane = pixel p, channels cho .. cho + 3
-            const long long row = (long long)q0 * V + p;
-            const bool st = p < TPX && q < QO;
-            f32x4 v = acc;
-            if constexpr (RAW) {
-                v += bv;
+                if (s < 5) continue;
+                // epilogue of block b: lane = pixel p, channels cho .. cho + 3
+                const int p = (blk0 + b) * 16 + (lane & 15);
+                const int fo = p / V;
+                const int q = q0 + fo;
+                const long long row = (long long)q0 * V + p;
+                const bool st = p < TPX && q < QO;
+                f32x4 v = acc;
+                acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (RAW) {
+                    v += bv;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    v[e] += res[b][0] * rw[e][0] + res[b][1] * rw[e][1] + res[b][2] * rw[e][2] + res[b][3] * rw[e][3];
-                    v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] += res[b][0] * rw[e][0] + res[b][1] * rw[e][1] + res[b][2] * rw[e][2] + res[b][3] * rw[e][3];
+                        v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    }
+                    xbf16x8 p0, p1, p2;
+                    xsplit8(v, v, p0, p1, p2);
+                    typedef __bf16 xbf16x4 __attribute__((ext_vector_type(4)));
+                    unsigned short* o = st ? a.out_p3 + row * (3 * C) + cho : reinterpret_cast<unsigned short*>(a.trash);
+                    *reinterpret_cast<xbf16x4*>(o) = xbf16x4{p0[0], p0[1], p0[2], p0[3]};
+                    *reinterpret_cast<xbf16x4*>(o + C) = xbf16x4{p1[0], p1[1], p1[2], p1[3]};
+                    *reinterpret_cast<xbf16x4*>(o + 2 * C) = xbf16x4{p2[0], p2[1], p2[2], p2[3]};
+                } else {
+                    v += res[b];   // (acc + x) + bias: xgemm's identity-epilogue order
+                    v += bv;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    float* o = st ? a.out_f + row * C + cho : a.trash;
+                    *reinterpret_cast<f32x4*>(o) = v;
                 }
-                xbf16x8 p0, p1, p2;
-                xsplit8(v, v, p0, p1, p2);
-                typedef __bf16 xbf16x4 __attribute__((ext_vector_type(4)));
-                unsigned short* o = st ? a.out_p3 + row * (3 * C) + cho : reinterpret_cast<unsigned short*>(a.trash);
-                *reinterpret_cast<xbf16x4*>(o) = xbf16x4{p0[0], p0[1], p0[2], p0[3]};
-                *reinterpret_cast<xbf16x4*>(o + C) = xbf16x4{p1[0], p1[1], p1[2], p1[3]};
-                *reinterpret_cast<xbf16x4*>(o + 2 * C) = xbf16x4{p2[0], p2[1], p2[2], p2[3]};
-            } else {
-                v += res[b];   // (acc + x) + bias: xgemm's identity-epilogue order
-                v += bv;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-                float* o = st ? a.out_f + row * C + cho : a.trash;
-                *reinterpret_cast<f32x4*>(o) = v;
             }
         }
         // every wave done reading the z image (and, block 0, the keypoint image)

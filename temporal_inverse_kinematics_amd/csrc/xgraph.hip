@@ -193,15 +193,20 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         lds_barrier();
         stamp(0);
         const unsigned char* P = pimg(s);
-        xbf16x8 xb[2][3];
+        // operand ring: joint j + XPF's planes are read while joint j's MFMAs run
+        // (a sched_barrier between the reads and the MFMAs: left alone, the
+        // scheduler sinks the reads next to their use and exposes the LDS latency)
+        constexpr int XPF = 2;
+        xbf16x8 xb[XPF + 1][3];
         auto rd = [&](int j, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(P + xg_unit(16 * j + f, p, g));
         };
         auto mfma_j = [&](int j) __attribute__((always_inline)) {
-            if (j + 1 < V) rd(j + 1, xb[(j + 1) & 1]);
+            if (j + XPF < V) rd(j + XPF, xb[(j + XPF) % (XPF + 1)]);
+            __builtin_amdgcn_sched_barrier(0);
             if (XG_OFF(4)) return;
-            const xbf16x8(&x)[3] = xb[j & 1];
+            const xbf16x8(&x)[3] = xb[j % (XPF + 1)];
             // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgemm's product order
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[kb][0], x[2], acc[j], 0, 0, 0);
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[kb][1], x[1], acc[j], 0, 0, 0);
@@ -211,7 +216,8 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[kb][0], x[0], acc[j], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         };
-        rd(0, xb[0]);
+#pragma unroll
+        for (int j = 0; j < XPF; ++j) rd(j, xb[j]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_j(j);
         stamp(1);

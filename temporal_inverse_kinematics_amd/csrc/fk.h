@@ -19,6 +19,7 @@ struct FkChainArgs {
     int arows;               // rows of ablk per body: 16 (rows 12..15 = [0 0 0 1]) or 12 (the 3x4 part only)
     unsigned short* feat_sb; // (B, kp/32 blocks of [hi x32 | lo x32]): feat split for the f16x3 GEMM (or null)
     unsigned short* ablk_sb; // (B*16, kj/32 blocks): ablk split likewise (or null)
+    float* ajt;              // (B,55,12) A_j joint-major for the sparse skinning kernel (or null)
     float* joints;           // (B,njoints,3): first 55 written here
     int* dyn_bin;            // (B) or null
     const int* depth;        // (55) depth of each joint in the kinematic tree (root 0)
@@ -39,6 +40,22 @@ struct FkSkinArgs {
     unsigned short* trash;           // >= 1 KB scratch: stores of rows past the batch
 };
 hipError_t launch_fk_skin(const FkSkinArgs& a, hipStream_t st);
+
+// The same LBS on the sparse skinning weights: T = sum over the (at most nz)
+// joints of vertex v with W[v][j] > 2^-30, in ascending joint order, in fp32
+// FMAs (the dense product's terms in its order, minus terms below 2^-30 of a
+// transform); one thread per vertex, a run of bodies per workgroup.
+struct FkSkinSpArgs {
+    int B, V, nz;                    // nz: entries per vertex (4, 8 or 16)
+    const float* ajt;                // (B,55,12) A_j, joint-major
+    const int2* nzw;                 // (V,nz) {joint, float bits of W[v][joint]}, joints ascending; padding {0, 0}
+    const float* vposed;             // (B, ldv) v_posed, 3V used
+    int ldv;
+    const float* transl;             // (B,3): a zero array when the caller has none
+    float* verts;                    // (B, 3V)
+    int ncu;
+};
+hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st);
 
 struct FkLmkArgs {
     int B, V, njoints, nextra, nlmk, ndyn;

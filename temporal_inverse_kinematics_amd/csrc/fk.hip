@@ -160,6 +160,12 @@ __global__ __launch_bounds__(64 * FKW) void fk_chain_kernel(FkChainArgs a) {
         for (int e = 0; e < ar; ++e)
             if (j < a.kj) G[e * a.kj + j] = A[e];
     }
+    if (a.ajt && j < 55) {   // joint-major: lane j writes its 12 entries
+        f32x4* o = reinterpret_cast<f32x4*>(a.ajt + ((size_t)b * 55 + j) * 12);
+        o[0] = f32x4{A[0], A[1], A[2], A[3]};
+        o[1] = f32x4{A[4], A[5], A[6], A[7]};
+        o[2] = f32x4{A[8], A[9], A[10], A[11]};
+    }
     if (a.ablk_sb) {   // rows b*16+e, K = joint: block j/32, hi at j%32, lo 32 further
         unsigned short* G = a.ablk_sb + (size_t)b * 16 * (2 * a.kj);
         for (int e = 0; e < 16; ++e) {
@@ -377,6 +383,119 @@ hipError_t launch_fk_skin(const FkSkinArgs& a, hipStream_t st) {
     runs = runs < nbt ? runs : nbt;
     (void)hipGetLastError();
     hipLaunchKernelGGL(fk_skin_kernel, dim3(vt, runs), dim3(512), 0, st, a, runs);
+    return hipGetLastError();
+}
+
+// Sparse skinning. A workgroup owns 256 consecutive vertices (thread = vertex,
+// its nz {joint, weight} pairs in registers) and walks a run of body tiles of
+// SBT = 4 bodies: the tile's A_j (SBT x 55 x 12 floats) sits in LDS, double
+// buffered — the next tile's A_j and v_posed rows are loaded into registers
+// during the current tile's math, written to the other buffer after it, one
+// barrier per tile. Loads and stores are 12 B per thread, consecutive across
+// lanes (vertex-major rows), so every wave moves 768 contiguous bytes.
+namespace fksp {
+constexpr int SBT = 4;                          // bodies per tile
+constexpr int AB = 55 * 12;                     // floats of A_j per body
+constexpr int ABUF = SBT * AB;                  // floats per buffer (10,560 B)
+constexpr int NA4 = (ABUF / 4 + 255) / 256;     // f32x4 loads per thread per tile (3)
+}  // namespace fksp
+
+template <int NZ>
+__global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int runs) {
+    using namespace fksp;
+    __shared__ __attribute__((aligned(16))) float sA[2][ABUF];
+    const int tid = threadIdx.x;
+    const int v = blockIdx.x * 256 + tid;
+    const bool vok = v < a.V;
+    const int vc = vok ? v : a.V - 1;
+    const int nbt = (a.B + SBT - 1) / SBT;
+    const int t0 = (int)((long long)blockIdx.y * nbt / runs), t1 = (int)((long long)(blockIdx.y + 1) * nbt / runs);
+    if (t0 >= t1) return;
+    int jo[NZ];
+    float wv[NZ];
+#pragma unroll
+    for (int k = 0; k < NZ; ++k) {
+        const int2 e = a.nzw[(size_t)vc * NZ + k];
+        jo[k] = e.x * 12;
+        wv[k] = __builtin_bit_cast(float, e.y);
+    }
+    f32x4 pa[NA4];
+    auto load = [&](int t, float (&pv)[SBT][3]) __attribute__((always_inline)) {   // tile t's A_j and v_posed into registers
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.ajt + (size_t)t * ABUF);
+        const int nb = min(SBT, a.B - t * SBT);
+#pragma unroll
+        for (int i = 0; i < NA4; ++i) {
+            const int q = tid + 256 * i;
+            pa[i] = q < nb * (AB / 4) ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int b = 0; b < SBT; ++b) {
+            const int body = min(t * SBT + b, a.B - 1);
+            __builtin_memcpy(&pv[b][0], a.vposed + (size_t)body * a.ldv + 3 * vc, 12);
+        }
+    };
+    auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NA4; ++i) {
+            const int q = tid + 256 * i;
+            if (q < ABUF / 4) reinterpret_cast<f32x4*>(sA[buf])[q] = pa[i];
+        }
+    };
+    auto tile = [&](int t, const float (&cv)[SBT][3], float (&nv)[SBT][3]) __attribute__((always_inline)) {
+        if (t + 1 < t1) load(t + 1, nv);
+        const float* A = sA[t & 1];
+#pragma unroll
+        for (int b = 0; b < SBT; ++b) {
+            const int body = t * SBT + b;
+            const int bc = body < a.B ? body : a.B - 1;
+            float T[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) T[e] = 0.f;
+#pragma unroll
+            for (int k = 0; k < NZ; ++k) {
+                const f32x4* r = reinterpret_cast<const f32x4*>(A + b * AB + jo[k]);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const f32x4 x = r[q];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) T[4 * q + e] = fmaf(wv[k], x[e], T[4 * q + e]);
+                }
+                if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // at most four joints' reads in flight
+            }
+            float o[3];
+#pragma unroll
+            for (int g = 0; g < 3; ++g)
+                o[g] = fmaf(T[4 * g], cv[b][0], fmaf(T[4 * g + 1], cv[b][1], fmaf(T[4 * g + 2], cv[b][2], T[4 * g + 3]))) +
+                       a.transl[bc * 3 + g];
+            if (vok && body < a.B) __builtin_memcpy(a.verts + (size_t)body * 3 * a.V + 3 * v, o, 12);
+            __builtin_amdgcn_sched_barrier(0);   // one body's LDS reads in flight at a time (registers)
+        }
+        if (t + 1 < t1) put((t + 1) & 1);
+        __syncthreads();
+    };
+    float va[SBT][3], vb[SBT][3];
+    load(t0, va);
+    put(t0 & 1);   // tile t reads buffer t & 1
+    __syncthreads();
+    for (int t = t0; t < t1; t += 2) {   // unrolled by two: the v_posed buffers swap statically
+        tile(t, va, vb);
+        if (t + 1 < t1) tile(t + 1, vb, va);
+    }
+}
+
+hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st) {
+    if (a.B <= 0 || a.V <= 0) return hipSuccess;
+    if ((a.nz != 4 && a.nz != 8 && a.nz != 16) || !a.ajt || !a.nzw || !a.vposed || !a.verts || !a.transl || a.ldv < 3 * a.V)
+        return hipErrorInvalidValue;
+    const int vt = (a.V + 255) / 256, nbt = (a.B + fksp::SBT - 1) / fksp::SBT;
+    // about 4 workgroups per CU, each walking a run of body tiles
+    int runs = (4 * (a.ncu > 0 ? a.ncu : 256) + vt - 1) / vt;
+    runs = runs < nbt ? runs : nbt;
+    (void)hipGetLastError();
+    const dim3 grid(vt, runs);
+    if (a.nz == 4) hipLaunchKernelGGL(fk_skin_sparse_kernel<4>, grid, dim3(256), 0, st, a, runs);
+    else if (a.nz == 8) hipLaunchKernelGGL(fk_skin_sparse_kernel<8>, grid, dim3(256), 0, st, a, runs);
+    else hipLaunchKernelGGL(fk_skin_sparse_kernel<16>, grid, dim3(256), 0, st, a, runs);
     return hipGetLastError();
 }
 

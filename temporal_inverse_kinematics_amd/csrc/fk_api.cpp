@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -44,12 +45,16 @@ struct tik_fk {
     bool skin12 = true;   // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=0: 16)
     int ncu = 256;
     int prec = 1;
+    // sparse skinning (fk.hip fk_skin_sparse_kernel): per vertex the joints with
+    // W > 2^-30 as {joint, weight} pairs, sp_nz per vertex (0: off, TIK_FK_SPARSE=0)
+    DevIBuf nzw;
+    int sp_nz = 0;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
     DevIBuf parents, chain, faces, lmk_faces, dyn_faces, extra, depth;
     int nchain = 0, maxdepth = 0;
     int ldv = 0;       // v_posed row stride (3V rounded up to 4 floats: vector stores)
     // workspace
-    DevBuf feat, ablk, vposed, verts_ws;
+    DevBuf feat, ablk, vposed, verts_ws, ajt;
     DevHBuf feat_sb, ablk_sb, trash;
     DevBuf zero_transl;   // (B,3) zeros: the skinning kernel always reads a translation
     DevIBuf dyn_bin;
@@ -184,6 +189,36 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         delete fk;
         return rc;
     }
+    {   // sparse skinning weights
+        const float tau = std::ldexp(1.0f, -30);
+        int nzmax = 0;
+        for (int v = 0; v < V; ++v) {
+            int n = 0;
+            for (int j = 0; j < NJ; ++j) n += lw->v[(size_t)v * NJ + j] > tau ? 1 : 0;
+            nzmax = std::max(nzmax, n);
+        }
+        const int nz = nzmax <= 4 ? 4 : nzmax <= 8 ? 8 : nzmax <= 16 ? 16 : 0;
+        const char* e = getenv("TIK_FK_SPARSE");
+        if (nz && !(e && e[0] == '0')) {
+            std::vector<int> h((size_t)V * nz * 2, 0);
+            for (int v = 0; v < V; ++v) {
+                int n = 0;
+                for (int j = 0; j < NJ; ++j) {
+                    const float w = lw->v[(size_t)v * NJ + j];
+                    if (w > tau) {
+                        h[((size_t)v * nz + n) * 2] = j;
+                        std::memcpy(&h[((size_t)v * nz + n) * 2 + 1], &w, 4);
+                        ++n;
+                    }
+                }
+            }
+            if ((rc = fk->nzw.upload(h))) {
+                delete fk;
+                return rc;
+            }
+            fk->sp_nz = nz;
+        }
+    }
     if (const char* e = getenv("TIK_FK_PT")) fk->xpt = e[0] != '0';
     if (const char* e = getenv("TIK_FK_SKIN12")) fk->skin12 = e[0] != '0';
     {
@@ -235,6 +270,7 @@ int tik_fk_reserve(tik_fk_t fk, int B) {
     if ((rc = fk->feat.reserve((size_t)B * KP)) || (rc = fk->ablk.reserve((size_t)B * 16 * KJ)) ||
         (rc = fk->feat_sb.reserve((size_t)B * 2 * KP)) || (rc = fk->ablk_sb.reserve((size_t)B * 16 * 2 * KJ)) ||
         (rc = fk->vposed.reserve((size_t)B * fk->ldv)) || (rc = fk->dyn_bin.reserve((size_t)B)) ||
+        (fk->sp_nz && (rc = fk->ajt.reserve((size_t)B * 55 * 12))) ||
         (rc = fk->zero_transl.upload(std::vector<float>((size_t)B * 3, 0.f))) ||
         (!fk->trash.p && (rc = fk->trash.upload(std::vector<unsigned short>(4096, 0)))))
         return rc;
@@ -258,7 +294,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     c.B = B; c.nb = fk->nb; c.ne = fk->ne; c.kp = KP; c.kj = KJ; c.njoints = fk->njoints; c.nchain = fk->nchain;
     c.pose = full_pose; c.betas = betas; c.expr = expression; c.transl = transl; c.pose_mean = fk->pose_mean.p;
     c.parents = fk->parents.p; c.chain = fk->chain.p; c.jt = fk->jt.p; c.jd = fk->jd.p;
-    c.feat = f16x3 ? nullptr : fk->feat.p; c.ablk = f16x3 ? nullptr : fk->ablk.p;
+    const bool sparse = !f16x3 && fk->sp_nz > 0;
+    c.feat = f16x3 ? nullptr : fk->feat.p; c.ablk = f16x3 || sparse ? nullptr : fk->ablk.p;
+    c.ajt = sparse ? fk->ajt.p : nullptr;
     // rows of A_j per body in ablk: the persistent bf16x3 skinning GEMM skips the [0 0 0 1] row
     const int ar = fk->prec == tik::PREC_BF16X3 && fk->xWT.p && fk->xpt && fk->skin12 ? 12 : 16;
     c.arows = ar;
@@ -308,7 +346,19 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
         }
 
-        if (fk->prec == tik::PREC_BF16X3 && fk->xWT.p) {
+        if (sparse) {
+            // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
+            tik::FkSkinSpArgs s{};
+            s.B = B; s.V = fk->V; s.nz = fk->sp_nz; s.ajt = fk->ajt.p;
+            s.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
+            s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
+            s.ncu = fk->ncu;
+            // algorithmic: nz joints x 12 entries + the 3x4 vertex transform per (body, vertex);
+            // bytes: A_j in, v_posed in, vertices out, the pairs once
+            ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
+                         4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + 2.0 * Vd * fk->sp_nz), st);
+            HIP_TRY(tik::launch_fk_skin_sparse(s, st));
+        } else if (fk->prec == tik::PREC_BF16X3 && fk->xWT.p) {
             // skinning + vertex transform on xgemm.hip (EPI_SKIN)
             tik::XArgs s{};
             s.M = B * ar; s.Nc = fk->V; s.V = 1; s.tout = B * ar;

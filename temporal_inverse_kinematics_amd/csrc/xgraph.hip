@@ -61,10 +61,8 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
     using namespace xg;
     constexpr int D = NK <= 4 ? 2 : 1;   // steps of prefetch in registers (NK = 8: the weights take 96 VGPRs)
     constexpr int B2MAX = V * 256 * 4;
-    constexpr int ATLD = 20;   // A_eff^T rows (17 coefficients + pad: five b128 broadcast reads)
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PBYTES + B2MAX + V * ATLD * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PBYTES + B2MAX];
     float* const b2s = reinterpret_cast<float*>(smem + 2 * PBYTES);
-    float* const ats = reinterpret_cast<float*>(smem + 2 * PBYTES + B2MAX);
     auto pimg = [&](int s) __attribute__((always_inline)) { return smem + (s & 1) * PBYTES; };
 
     int tid = threadIdx.x, lane = tid & 63;
@@ -88,12 +86,11 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
     auto tile_fg = [&](int t) __attribute__((always_inline)) { return t / npass; };
     auto tile_pass = [&](int t) __attribute__((always_inline)) { return t - (t / npass) * npass; };
 
-    // bias2 [17][cout] and A_eff^T [w][v] in LDS (the mix reads coefficients as broadcasts)
+    // bias2 [17][cout] in LDS, A_eff in VGPRs (v_readlane)
     for (int i = tid; i < V * a.cout; i += 512) b2s[i] = a.bias2[i];
-    for (int i = tid; i < V * ATLD; i += 512) {
-        const int wj = i / ATLD, v = i - wj * ATLD;
-        ats[i] = v < V ? a.amix[v * V + wj] : 0.f;
-    }
+    float amv[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) amv[k] = 64 * k + lane < V * V ? a.amix[64 * k + lane] : 0.f;
 
     // ---- the fp32 rows of global step s (tile t_begin + s / NK, K block s % NK):
     // unit U = 512 i + tid: group row m = U / 8 (frame m / 17, joint m % 17), channels 4 (U % 8) ..
@@ -187,12 +184,6 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
 
     // one K step; KB compile-time so the weights and the prefetch registers are
     // statically indexed (s % D == KB % D: NK is even)
-    // The split + loads of the next step go after joint 3's MFMAs on waves 0-3 and
-    // after joint 11's on waves 4-7: the two waves of a SIMD are at different
-    // places, so one splits while the other issues MFMAs (both at the same place
-    // would leave the MFMA pipe idle meanwhile). A uniform branch at both sites,
-    // not two copies of the loop (that doubles the live ranges across them).
-    const bool early = wave < 4;
     auto step = [&](int s, int t, int pass, auto KBc) __attribute__((always_inline)) {
         constexpr int kb = decltype(KBc)::value;
         constexpr int nb = (kb + 1) % D;   // registers holding step s+1
@@ -205,7 +196,7 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         // operand ring: joint j + XPF's planes are read while joint j's MFMAs run
         // (a sched_barrier between the reads and the MFMAs: left alone, the
         // scheduler sinks the reads next to their use and exposes the LDS latency)
-        constexpr int XPF = NK == 8 ? 1 : 2;   // NK = 8: the weights take 96 VGPRs
+        constexpr int XPF = 2;
         xbf16x8 xb[XPF + 1][3];
         auto rd = [&](int j, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
 #pragma unroll
@@ -227,23 +218,15 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         };
 #pragma unroll
         for (int j = 0; j < XPF; ++j) rd(j, xb[j]);
-        auto split_next = [&]() __attribute__((always_inline)) {
-            stamp(1);
-            if (!XG_OFF(2)) split(s + 1, rb[nb]);   // VALU + LDS writes beside the MFMAs (past the run: zeros, never read)
-            stamp(2);
-        };
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            mfma_j(j);
-            if (j == 3 && early) split_next();
-            if (j == 11 && !early) split_next();
-            // the loads into the registers just split: the same place on every wave
-            // (outside the branches, so the compiler's vmcnt accounting stays exact)
-            if (j == 11) {
-                load(s + 1 + D, rb[nb]);
-                stamp(3);
-            }
-        }
+        for (int j = 0; j < 4; ++j) mfma_j(j);
+        stamp(1);
+        if (!XG_OFF(2)) split(s + 1, rb[nb]);   // VALU + LDS writes beside the MFMAs (past the run: zeros, never read)
+        stamp(2);
+        load(s + 1 + D, rb[nb]);
+        stamp(3);
+#pragma unroll
+        for (int j = 4; j < V; ++j) mfma_j(j);
         stamp(4);
         if constexpr (NP == 2) load_wk(tile_pass(t + 1), kb);
         if constexpr (kb == NK - 1) {
@@ -255,21 +238,19 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
 #pragma unroll
                 for (int wj = 0; wj < V; ++wj) {
                     f32x4 z = *reinterpret_cast<const f32x4*>(b2s + wj * a.cout + co);
-                    f32x4 cf[ATLD / 4];
-#pragma unroll
-                    for (int i = 0; i < ATLD / 4; ++i) cf[i] = *reinterpret_cast<const f32x4*>(ats + wj * ATLD + 4 * i);
 #pragma unroll
                     for (int v = 0; v < V; ++v)
                         if (XG_OFF(16)) {
                             if (v == wj) z += acc[v];
                         } else if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
-                            z += cf[v >> 2][v & 3] * acc[v];
+                            const float av = __builtin_bit_cast(
+                                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + wj) / 64]), (v * V + wj) % 64));
+                            z += av * acc[v];
                         }
 #pragma unroll
                     for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
                     float* o = q < QO ? a.out + ((size_t)q * V + wj) * a.ldo + co : a.trash;
                     if (!XG_OFF(8)) xst4(o, z, a.nts);
-                    __builtin_amdgcn_sched_barrier(0);   // one output joint's coefficient reads at a time
                 }
             };
             if (a.mix_sparse) mix_all(std::true_type{});

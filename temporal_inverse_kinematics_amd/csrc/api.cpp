@@ -30,6 +30,7 @@
 #include "xblock.h"
 #include "xgemm.h"
 #include "xgraph.h"
+#include "xtconv.h"
 
 namespace tik_host {
 thread_local std::string g_err;
@@ -227,6 +228,7 @@ struct Layer {
     SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
+    DevHBuf xtw;            // resident-weight temporal conv (xtconv.hip, 128 -> 128, stride 1, identity residual)
     DevHBuf xgw;            // weight-stationary gcn kernel (xgraph.hip, 128 / 256 output channels): gcn planes in the MFMA register layout
     DevHBuf xbg, xbt;       // whole-block kernel (xblock.hip, 64 channels, stride 1): gcn / tcn planes in the MFMA register layout
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
@@ -234,6 +236,7 @@ struct Layer {
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers)
+    int xtcon = 0;          // temporal conv on xtconv.hip where packed (TIK_XTC bit mask of layers; off: measured 1-2 % slower than XT128)
     int xws = 0;            // 128-column temporal convs on the warp-specialized persistent kernel (launch_xgemm_ws; TIK_XWS bit mask of layers; off: measured 3-9 % slower)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
@@ -315,6 +318,8 @@ struct Layer {
                 if ((rc = xt.upload(tik::xgemm_pack(t, ns, cout, bn)))) return rc;
                 xt_bn = bn; xt_ks = TK * cout / 32 + (ns == 2 ? cin / 32 : 0);
             }
+            if (cout == 128 && cin == 128 && stride == 1 && res == RES_IDEN && V == 17)   // xtconv.hip
+                if ((rc = xtw.upload(tik::xblock_pack_weights(hwt.data(), cout, TK * cout, TK, cout)))) return rc;
             if ((cout == 128 || cout == 256) && (cin == 64 || cin == 128 || cin == 256) && V == 17)   // xgraph.hip
                 if ((rc = xgw.upload(tik::xblock_pack_weights(hwg.data(), cout, cinp, 1, cin)))) return rc;
             if (cout == 64 && stride == 1 && V == 17) {   // xblock.hip
@@ -424,6 +429,17 @@ struct Layer {
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
+        }
+        if (xtcon && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0) {
+            tik::XTConvArgs c{};
+            c.M = (int)rout; c.T = tin; c.z = z; c.ldz = cout; c.x = x; c.ldx = ld; c.wp = xtw.p; c.bias = biasT.p;
+            c.out = out; c.ldo = cout; c.nts = xnts(index); c.trash = xtrash; c.tune = xtune();
+            const std::string lab = "XTC.L" + std::to_string(index);
+            ProfScope p(lab.c_str(), 2.0 * px_out * TK * cout * cout,
+                        4.0 * (px_in * cout + 2.0 * px_out * cout + (double)TK * cout * cout), st);
+            p.out(out, (size_t)rout * cout * 4);
+            HIP_TRY(tik::launch_xtconv(c, ncu, st));
+            return TIK_OK;
         }
         tik::XArgs t{};
         t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
@@ -853,6 +869,7 @@ static void apply_env(tik_model* md) {
             L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
             if (const char* w = getenv("TIK_XWS")) L.xws = (atoi(w) >> L.index) & 1;
             if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
+            if (const char* w = getenv("TIK_XTC")) L.xtcon = (atoi(w) >> L.index) & 1;
             L.xtrash = reinterpret_cast<float*>(md->trash.p);
         }
     }

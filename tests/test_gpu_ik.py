@@ -615,3 +615,23 @@ def test_xgraph_vs_tiled(n, T):
         b = tl(x)["poses"]
     assert torch.isfinite(a).all()
     assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (2, 9), (1, 1), (5, 31)])
+def test_xtconv_vs_tiled(n, T):
+    """The temporal conv of the 128-channel stride-1 blocks as the
+    resident-weight persistent kernel (xtconv.hip: weights in LDS, activations
+    straight into registers; opt-in, TIK_XTC) against the tiled XT128 kernel
+    (TIK_XTC=0): the same bf16x3 products in the same K order and the same
+    (acc + x) + bias epilogue, so the poses are bit-identical — at the bench
+    size, partial last row blocks, short windows (taps at both edges), single
+    frames and T=65."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    xt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=255)
+    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=0)
+    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n * 3 + T)).cuda()
+    with torch.no_grad():
+        a = xt(x)["poses"].clone()
+        b = tl(x)["poses"]
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).abs().max())

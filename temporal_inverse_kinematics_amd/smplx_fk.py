@@ -122,14 +122,27 @@ class SMPLX:
         return self
 
     def full_forward(self, full_pose: torch.Tensor, betas=None, expression=None, transl=None,
-                     return_verts: bool = True):
-        """full_pose (B,55,3) device -> (joints (B,J,3), vertices (B,V,3) or None)."""
+                     return_verts: bool = True, out=None):
+        """full_pose (B,55,3) device -> (joints (B,J,3), vertices (B,V,3) or None).
+        out: optional preallocated (joints, vertices) float32 tensors of those
+        shapes to write into (a serving loop's output buffers; vertices may be None)."""
         fp = full_pose.reshape(-1, 55, 3).contiguous()
         B = fp.shape[0]
         args = [t.contiguous() if t is not None else None for t in (betas, expression, transl)]
         _lib.require_gpu(fp, *args)
-        joints = torch.empty((B, self.num_joints, 3), device=fp.device, dtype=torch.float32)
-        verts = torch.empty((B, self.num_verts, 3), device=fp.device, dtype=torch.float32) if return_verts else None
+        if out is not None:
+            joints, verts = out
+            if joints.shape != (B, self.num_joints, 3) or not joints.is_contiguous() or joints.dtype != torch.float32:
+                raise ValueError("out joints must be a contiguous float32 (B, num_joints, 3) tensor")
+            if verts is not None and (verts.shape != (B, self.num_verts, 3) or not verts.is_contiguous()
+                                      or verts.dtype != torch.float32):
+                raise ValueError("out vertices must be a contiguous float32 (B, num_verts, 3) tensor")
+            if not return_verts:
+                verts = None
+            _lib.require_gpu(joints, verts)
+        else:
+            joints = torch.empty((B, self.num_joints, 3), device=fp.device, dtype=torch.float32)
+            verts = torch.empty((B, self.num_verts, 3), device=fp.device, dtype=torch.float32) if return_verts else None
         _lib.check(_lib.load().tik_fk_forward(self._h, fp.data_ptr(), _lib.ptr(args[0]), _lib.ptr(args[1]),
                                               _lib.ptr(args[2]), B, joints.data_ptr(), _lib.ptr(verts),
                                               _lib.stream_of(fp)), "SMPLX.forward")

@@ -239,3 +239,18 @@ def test_run_smpl_inference_api(consts):
     b = np.tile(np.asarray(data["betas"], np.float32)[:10][None], (F, 1))
     jr2 = sl.smplx_forward(syn.synthetic_smplx_constants(seed=1), full, b, transl=data["trans"], return_verts=False)
     assert np.abs(jt - jr2).max() < TOL
+
+
+def test_fk_out_buffers(consts, model):
+    """full_forward(out=(joints, vertices)) writes the same values into the
+    caller's buffers (the FK bench's serving-loop form) and returns them; wrong
+    shapes are refused."""
+    pose, betas, expr, transl = _inputs(6, 321)
+    cu = lambda a: torch.from_numpy(a).cuda()
+    j, v = model.full_forward(cu(pose), cu(betas), cu(expr), cu(transl))
+    oj, ov = torch.full_like(j, 7.0), torch.full_like(v, 7.0)
+    j2, v2 = model.full_forward(cu(pose), cu(betas), cu(expr), cu(transl), out=(oj, ov))
+    assert j2.data_ptr() == oj.data_ptr() and v2.data_ptr() == ov.data_ptr()
+    assert torch.equal(oj, j) and torch.equal(ov, v)
+    with pytest.raises(ValueError):
+        model.full_forward(cu(pose), out=(oj[:5], ov))

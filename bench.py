@@ -419,7 +419,7 @@ def main():
             # BASELINE configs #4 and #5 under the same clock (the headline stays config #2)
             from bench_fk import measure_fk
             from bench_stream import measure_online
-            out["fk"] = measure_fk(batch=4096, steps=10, warmup=3)
+            out["fk"] = measure_fk(batch=4096, steps=10, warmup=20)
             out["online"] = measure_online(frames=2000, warmup=100, win=T)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = _cpu_baseline(T, args.cpu_seconds)

@@ -17,7 +17,7 @@ DTYPES = {"bf16x3": "f32 via bf16x3 (3 bf16 planes, 6 MFMA products, fp32 accumu
           "fp32": "f32 (exact fp32 MFMA)"}
 
 
-def measure_fk(batch=4096, steps=10, warmup=3):
+def measure_fk(batch=4096, steps=10, warmup=20):
     """Time `steps` FK+LBS forwards of `batch` bodies (inputs resident), then the
     same steps again with per-launch HIP events: the step time and the per-kernel
     roofline of the two LBS GEMMs (bf16x3: 6 bf16 MFMA products per fp32 product)."""
@@ -29,8 +29,9 @@ def measure_fk(batch=4096, steps=10, warmup=3):
     m = SMPLX(c, batch_size=batch)
     pose, betas = syn.synthetic_fk_inputs(batch, seed=1)
     P, Bt = torch.from_numpy(pose).cuda(), torch.from_numpy(betas).cuda()
-    # outputs into preallocated buffers (a serving loop's): a fresh 515 MB vertex
-    # tensor per step alternates two allocator blocks and costs ~0.1 ms of the step
+    # outputs into preallocated buffers (a serving loop's); 20 warmup steps: the
+    # first ~10 FK steps on a fresh box run 5-20 % slow (clocks / caches settling,
+    # scripts/diag_fkgap.py: 1.16 -> 0.98 ms/step)
     out = (torch.empty((batch, m.num_joints, 3), device="cuda"), torch.empty((batch, m.num_verts, 3), device="cuda"))
     for _ in range(warmup):
         m.full_forward(P, Bt, out=out)
@@ -87,7 +88,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     a = ap.parse_args()
     from temporal_inverse_kinematics_amd import synthetic as syn

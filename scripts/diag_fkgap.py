@@ -45,9 +45,10 @@ def direct():
 
 
 s = torch.cuda.Stream()
-print(f"full_forward default stream {run(ff, torch.cuda.default_stream()):.4f} ms")
-print(f"full_forward created stream {run(ff, s):.4f} ms")
-print(f"full_forward out= default  {run(ffo, torch.cuda.default_stream()):.4f} ms")
-print(f"full_forward out= created  {run(ffo, s):.4f} ms")
-print(f"direct      default stream {run(direct, torch.cuda.default_stream()):.4f} ms")
-print(f"direct      created stream {run(direct, s):.4f} ms")
+for rep in range(2):
+    print(f"[pass {rep}]")
+    print(f"direct      default stream {run(direct, torch.cuda.default_stream()):.4f} ms")
+    print(f"full_forward out= default  {run(ffo, torch.cuda.default_stream()):.4f} ms")
+    print(f"full_forward default stream {run(ff, torch.cuda.default_stream()):.4f} ms")
+    print(f"direct      created stream {run(direct, s):.4f} ms")
+    print(f"direct x50  default stream {run(direct, torch.cuda.default_stream(), 50):.4f} ms")

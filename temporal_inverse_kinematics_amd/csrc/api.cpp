@@ -461,10 +461,6 @@ struct Layer {
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
         t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.nts = xnts(index);
-        {
-            static const int stg = getenv("TIK_XPT_STAGGER") ? atoi(getenv("TIK_XPT_STAGGER")) : 0;   // experiment
-            t.pt_stagger = stg;
-        }
         t.trash = xtrash;
         const bool ws = xws && xtrash && xt_bn == 128 && xnw != 8 && !(res == RES_IDEN && !t.idn_epi) && tik::xgemm_ws_ok(t);
         const bool pt = !ws && xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);

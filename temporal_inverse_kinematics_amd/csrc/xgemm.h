@@ -62,7 +62,6 @@ struct XArgs {
     int idn_epi;  // with epi_lds: the identity residual added in the epilogue from row-major loads (no K steps)
     int epi_lds;  // EPI_BIAS: stage the C tile through LDS for whole-line row-major stores (else float4 stores from registers)
     int nw;     // waves per workgroup: 4 (or 0: two 128-row workgroups per CU) or 8 (one 256-row workgroup)
-    int pt_stagger;   // experiment (TIK_XPT_STAGGER): in xgemm_pt, the second half of the grid sleeps pt_stagger x 64 cycles first
     int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA, 8 skip the split
     unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null
 };

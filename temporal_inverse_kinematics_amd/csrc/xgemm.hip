@@ -665,8 +665,6 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
     const int G = gridDim.x, b = blockIdx.x;
     const int my = b < ntot ? (ntot - 1 - b) / G + 1 : 0;
     if (my == 0) return;
-    if (a.pt_stagger > 0 && b >= G / 2)   // experiment: offset the CU's second workgroup (persists across its tiles)
-        for (int i = 0; i < a.pt_stagger; ++i) __builtin_amdgcn_s_sleep(1);
     const int K = xgemm_kmain(a);                       // K steps per tile (all with weights)
     const int total = my * K;
     // tile i of this workgroup -> (first row, column tile): XCD-aware order over

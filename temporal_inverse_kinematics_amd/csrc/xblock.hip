@@ -261,17 +261,20 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             stamp(0);
-            if (wave >= 4) load_wt();
-            if (wave < 4) {
-                // G transposed: y^T = Wg' x^T; pixel block j = joint j of the tile's frames
-                // (lane & 15 = frame slot; slots 12-15 re-read slots 0-3: broadcast, discarded)
+            // G transposed, split by joint halves: waves 0-3 joints 0-8, waves 4-7 joints
+            // 9-16 (channel group cg = wave & 3 on both); the halves swap accumulators
+            // through the z image (free until the mix writes it), then each half mixes
+            // its own output joints. Same MFMAs and mix order as one wave doing all 17.
+            auto run_half = [&](auto jhc) __attribute__((always_inline)) {
+                constexpr int JH = decltype(jhc)::value, J0 = JH ? 9 : 0, J1 = JH ? V : 9;
                 f32x4 acc[V];
 #pragma unroll
                 for (int j = 0; j < V; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
                 const int fs = lane & 15, fr = fs < FIN ? fs : fs - FIN;
-                // operand ring: step s + XPF's planes are read while step s's MFMAs run (the
-                // sched_barrier keeps the scheduler from sinking the reads next to their use)
-                constexpr int XPF = 2;
+                // pixel block j = joint j of the tile's frames (lane & 15 = frame slot;
+                // slots 12-15 re-read slots 0-3: broadcast, discarded). Operand ring: step
+                // s + XPF's planes are read while step s's MFMAs run
+                constexpr int XPF = 2, S0 = 2 * J0, S1 = 2 * J1;
                 xbf16x8 xb[XPF + 1][3];
                 auto rd = [&](int s, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
                     const int R = (s >> 1) * FIN + fr, kb = s & 1;
@@ -279,13 +282,13 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                     for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(ximg + xb_unit(R, p, 4 * kb + g));
                 };
 #pragma unroll
-                for (int s = 0; s < XPF; ++s) rd(s, xb[s]);
+                for (int s = S0; s < S0 + XPF; ++s) rd(s, xb[(s - S0) % (XPF + 1)]);
 #pragma unroll
-                for (int s = 0; s < 2 * V; ++s) {
+                for (int s = S0; s < S1; ++s) {
                     const int j = s >> 1, kb = s & 1;
-                    if (s + XPF < 2 * V) rd(s + XPF, xb[(s + XPF) % (XPF + 1)]);
+                    if (s + XPF < S1) rd(s + XPF, xb[(s + XPF - S0) % (XPF + 1)]);
                     __builtin_amdgcn_sched_barrier(0);
-                    const xbf16x8(&x)[3] = xb[s % (XPF + 1)];
+                    const xbf16x8(&x)[3] = xb[(s - S0) % (XPF + 1)];
                     // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgemm's product order
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[2], acc[j], 0, 0, 0);
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][1], x[1], acc[j], 0, 0, 0);
@@ -295,14 +298,25 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[0], acc[j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                load_wt();   // its latency hides under the mix
-                // graph mix in registers: lane = frame fs, channels cho .. cho + 3, all 17 joints
-                // (xgemm.hip xmix_store's order: bias2, then v ascending)
+                load_wt();   // its latency hides under the exchange and the mix
+                // exchange: [joint][cg][lane] f32x4 in the z image rows (69.6 KB, below the zero row)
+                f32x4* xch = reinterpret_cast<f32x4*>(zimg);
+#pragma unroll
+                for (int j = J0; j < J1; ++j) xch[(j * 4 + cg) * 64 + lane] = acc[j];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    if (j < J0 || j >= J1) acc[j] = xch[(j * 4 + cg) * 64 + lane];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();   // every wave's exchange reads done before the z image writes
+                // graph mix in registers: lane = frame fs, channels cho .. cho + 3, output
+                // joints J0 .. J1 (xgemm.hip xmix_store's order: bias2, then v ascending)
                 if (fs < FIN) {
-                    auto mix_all = [&](auto sparse) __attribute__((always_inline)) {
+                    auto mix_half = [&](auto sparse) __attribute__((always_inline)) {
                         constexpr bool SP = decltype(sparse)::value;
 #pragma unroll
-                        for (int w = 0; w < V; ++w) {
+                        for (int w = J0; w < J1; ++w) {
                             f32x4 z = *reinterpret_cast<const f32x4*>(b2s + w * C + cho);
 #pragma unroll
                             for (int v = 0; v < V; ++v)
@@ -322,10 +336,13 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                             *reinterpret_cast<xbf16x4*>(zimg + xb_unit(R, 2, u) + o) = xbf16x4{p2[0], p2[1], p2[2], p2[3]};
                         }
                     };
-                    if (a.mix_sparse) mix_all(std::true_type{});
-                    else mix_all(std::false_type{});
+                    if (a.mix_sparse) mix_half(std::true_type{});
+                    else mix_half(std::false_type{});
                 }
-            }
+            };
+            // (both halves run the same number of s_barrier)
+            if (ph == 0) run_half(std::integral_constant<int, 0>{});
+            else run_half(std::integral_constant<int, 1>{});
         }
         stamp(1);
         __syncthreads();   // z image complete

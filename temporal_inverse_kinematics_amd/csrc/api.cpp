@@ -1183,26 +1183,26 @@ static hipError_t launch_xblock_traced(tik::XBlkArgs a, bool raw, int ncu, hipSt
     static const bool on = getenv("TIK_X_TRACE") != nullptr;
     if (!on) return tik::launch_xblock(a, raw, ncu, st);
     unsigned long long* d = nullptr;
-    hipError_t e = hipMalloc(&d, (size_t)ncu * 16 * 8);
+    hipError_t e = hipMalloc(&d, (size_t)ncu * 24 * 8);
     if (e != hipSuccess) return e;
-    (void)hipMemset(d, 0, (size_t)ncu * 16 * 8);
+    (void)hipMemset(d, 0, (size_t)ncu * 24 * 8);
     a.trace = d;
     e = tik::launch_xblock(a, raw, ncu, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    std::vector<unsigned long long> h((size_t)ncu * 16);
+    std::vector<unsigned long long> h((size_t)ncu * 24);
     if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d);
-    double s0[6] = {0}, s4[6] = {0}, nt = 0, n = 0;
+    double s0[8] = {0}, s4[8] = {0}, nt = 0;
     for (int w = 0; w < ncu; ++w) {
-        if (!h[16 * w + 7]) continue;
-        n += 1; nt += (double)h[16 * w + 6];
-        for (int k = 0; k < 6; ++k) { s0[k] += (double)h[16 * w + k]; s4[k] += (double)h[16 * w + 8 + k]; }
+        if (!h[24 * w + 9]) continue;
+        nt += (double)h[24 * w + 8];
+        for (int k = 0; k < 8; ++k) { s0[k] += (double)h[24 * w + k]; s4[k] += (double)h[24 * w + 12 + k]; }
     }
     nt = std::max(1.0, nt);
-    fprintf(stderr, "XBTRACE %-8s tiles %6.0f | per tile, wave0: start %6.0f G+mix %6.0f zbar %6.0f res+dma %6.0f T %6.0f endbar %6.0f"
-            " | wave4: start %6.0f G+mix %6.0f zbar %6.0f res+dma %6.0f T %6.0f endbar %6.0f\n", label, nt,
-            s0[0] / nt, s0[1] / nt, s0[2] / nt, s0[3] / nt, s0[4] / nt, s0[5] / nt, s4[0] / nt, s4[1] / nt, s4[2] / nt,
-            s4[3] / nt, s4[4] / nt, s4[5] / nt);
+    fprintf(stderr, "XBTRACE %-8s tiles %6.0f | per tile, wave0: start %6.0f G+mix %6.0f zbar %6.0f res %6.0f bar+dma %6.0f T %6.0f endbar %6.0f"
+            " | wave4: start %6.0f G+mix %6.0f zbar %6.0f res %6.0f bar+dma %6.0f T %6.0f endbar %6.0f\n", label, nt,
+            s0[0] / nt, s0[1] / nt, s0[2] / nt, (s0[3] + s0[6]) / nt, s0[7] / nt, s0[4] / nt, s0[5] / nt, s4[0] / nt, s4[1] / nt,
+            s4[2] / nt, (s4[3] + s4[6]) / nt, s4[7] / nt, s4[4] / nt, s4[5] / nt);
     return e;
 }
 

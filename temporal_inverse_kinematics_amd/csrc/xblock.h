@@ -29,7 +29,7 @@ struct XBlkArgs {
     float* out_f;                // block 1: fp32 [rows][64]
     unsigned short* out_p3;      // block 0: P3 planes [rows][3][64]
     float* trash;                // >= 64 B: store target of pixels past the batch
-    unsigned long long* trace;   // debug (-DTIK_XTRACE build): 16 phase sums per workgroup, or null
+    unsigned long long* trace;   // debug (-DTIK_XTRACE build): 24 phase sums per workgroup, or null
 };
 
 // raw: block 0 from the keypoints (writes P3); else block 1 from P3 (writes fp32).

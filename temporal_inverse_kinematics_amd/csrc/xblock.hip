@@ -81,9 +81,9 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
     if (t_begin >= t_end) return;
 
     // ---- weights in registers (MFMA A operand: lane l = output channel 16 cg + (l & 15), K group l >> 4).
-    // Wt' (72 VGPRs) is re-loaded every tile (L2 hits) where the wave's G work ends,
-    // so it is live only during T: live through G too it would not fit beside G's
-    // 68 accumulators
+    // Wt' (72 VGPRs) stays resident: with the gcn split by joint halves a wave
+    // holds 9 joints' accumulators during G (36 VGPRs), so Wt' fits beside them
+    // (it was re-loaded every tile before, ~2k cycles of L2 traffic per tile)
     xbf16x8 wt[3][2][3];   // [tap][K block][plane]
     auto load_wt = [&]() __attribute__((always_inline)) {
         const unsigned short* wp = a.wtp;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
 #else
     constexpr bool tr = false;
 #endif
-    unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+    unsigned long long ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;   // 6 res reads, 7 barrier + next-tile DMA issue (block 1)
     auto stamp = [&](int i) __attribute__((always_inline)) {
         if (tr) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -185,6 +185,15 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             tlast = t;
         }
     };
+    load_wt();
+    // the compiler's own wait for the Wt' loads goes here (an opaque use), not
+    // inside the tile loop behind DMAs it would have to count
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(wt[k][kb][p]));
     for (int tile = t_begin; tile < t_end; ++tile) {
         const int q0 = tile * F;
         stamp(-1);
@@ -255,7 +264,6 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                     else mix_half(I0{}, I9{}, std::false_type{});
                 }
             }
-            load_wt();
         } else {
             // x image landed (every wave waits for its own DMA share, then the barrier)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -298,7 +306,6 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                     acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wg[kb][0], x[0], acc[j], 0, 0, 0);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                load_wt();   // its latency hides under the exchange and the mix
                 // exchange: [joint][cg][lane] f32x4 in the z image rows (69.6 KB, below the zero row)
                 f32x4* xch = reinterpret_cast<f32x4*>(zimg);
 #pragma unroll
@@ -373,20 +380,13 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             }
         }
         if constexpr (!RAW) {
-            // Wt' landed and every wave done with the x image; then the next tile's x
-            // image (with nothing else outstanding, so T's register operands never wait
-            // on the DMA: the compiler cannot count the DMA loop's instructions)
-            // (the compiler's own wait for the Wt' loads goes here, where they are used by
-            // an opaque asm, not after the DMAs in front of the first MFMA)
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(wt[k][kb][p]));
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __syncthreads();
+            // every wave done with the x image (LDS reads; T's register operands are
+            // resident, so nothing in T waits on this DMA); s_barrier alone:
+            // __syncthreads' release fence would wait for the previous T's stores
+            stamp(6);
+            lds_barrier();
             if (tile + 1 < t_end) issue_x(tile + 1);
+            stamp(7);
         }
         stamp(3);
 
@@ -471,9 +471,9 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
         stamp(5);
     }
     if (tr && lane == 0) {
-        unsigned long long* o = a.trace + 16 * (size_t)blockIdx.x + (wave == 4 ? 8 : 0);
-        for (int i = 0; i < 6; ++i) o[i] = ph_[i];
-        o[6] = t_end - t_begin; o[7] = 1;
+        unsigned long long* o = a.trace + 24 * (size_t)blockIdx.x + (wave == 4 ? 12 : 0);
+        for (int i = 0; i < 8; ++i) o[i] = ph_[i];
+        o[8] = t_end - t_begin; o[9] = 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

@@ -1,6 +1,6 @@
 """Config #4: SMPL-X full 55-joint FK + 10475-vertex LBS, batch=4096, 1 GPU.
 
-    python bench_fk.py [--batch 4096] [--steps 10] [--warmup 3]
+    python bench_fk.py [--batch 4096] [--steps 10] [--warmup 20]
 
 Prints one JSON line: bodies/s, and per kernel (HIP events around every launch
 of a second pass of the same steps, tik_fk_profile) the algorithmic TFLOP/s of

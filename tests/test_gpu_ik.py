@@ -2,6 +2,8 @@
 made by the reference and against the CPU oracle. Tolerance: 1e-4 abs on the
 66-d poses (BASELINE.json north_star); features/blocks 1e-4 abs on O(1-5)
 activations (fp32 MFMA, BN folded)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -635,3 +637,31 @@ def test_xtconv_vs_tiled(n, T):
         b = tl(x)["poses"]
     assert torch.isfinite(a).all()
     assert torch.equal(a, b), float((a - b).abs().max())
+
+
+def test_run_test_end_to_end_and_cli(tmp_path):
+    """inference.run_test (`/root/reference/inference.py:110-145`) end to end on
+    the reference's shipped moveai sample (data/sample_3d_poses/
+    dance_contemporary.npz: its joints_3d and joint_3d_names, kept in
+    tests/golden/keypoints.npz and written back here in the file's layout):
+    moveai -> COCO on the device, IK over every frame, against the goldens the
+    reference itself produced (keypoints.npz coco_seq, run_inference.npz
+    win64); then the same through the CLI (`python -m
+    temporal_inverse_kinematics_amd.inference file.npz --out poses.npy`)."""
+    import subprocess
+    import sys
+    from temporal_inverse_kinematics_amd.inference import run_test
+    k, r = golden("keypoints.npz"), golden("run_inference.npz")
+    src = tmp_path / "cam01_track00.npz"
+    np.savez(src, joints_3d=k["moveai_joints"].astype(np.float32), joint_3d_names=k["moveai_names"])
+    out = run_test(str(src), win_size=64)
+    assert np.array_equal(out["coco"], k["coco_seq"].astype(np.float32))
+    assert out["poses"].shape == (231, 66) and np.isfinite(out["poses"]).all()
+    assert np.abs(out["poses"] - r["win64"]).max() < TOL
+    dst = tmp_path / "poses.npy"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "temporal_inverse_kinematics_amd.inference", str(src), "--out", str(dst)],
+                       cwd=root, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "solved 231 frames" in p.stdout
+    assert np.array_equal(np.load(dst), out["poses"])

@@ -69,8 +69,6 @@ def kernel_symbol(label, precision):
         return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
     if label in ("XB0", "XB1"):
         return f"tik::xblock_kernel<{'true' if label == 'XB0' else 'false'}>"
-    if label == "XW128":
-        return "tik::xgemm_ws_kernel"   # <identity residual>: the label does not say which (any instantiation)
     if label[:2] == "XP" and label[2:] in ("64", "128"):
         # xgemm_pt_kernel<BN, identity, residual conv>: the label does not say which (any instantiation)
         return "tik::xgemm_pt_kernel"

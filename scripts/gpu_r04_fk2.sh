@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fk.py > gpurun_out/fk_pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/fk_pytest.log
 [ $rc -eq 0 ] || exit $rc
-for cfg in "-" "TIK_FK_SBT=8" "TIK_FK_NT=1" "TIK_FK_SBT=8 TIK_FK_NT=1"; do
+for cfg in "-" "TIK_FK_SPARSE=0"; do
   envs=""; [ "$cfg" != "-" ] && envs="$cfg"
   env $envs timeout -k 10 200 python bench_fk.py --cpu-seconds 0 > gpurun_out/fk_ab.json 2> gpurun_out/fk_ab.err || { tail -5 gpurun_out/fk_ab.err; exit 3; }
   python - gpurun_out/fk_ab.json "$cfg" <<'PY'

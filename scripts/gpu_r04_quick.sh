@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out; TAG=${1:-q}; KEXPR=${2:-xgemm_ws}
+OUT=gpurun_out; TAG=${1:-q}; KEXPR=${2:-xgraph}
 shift 2 || true
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$KEXPR" > $OUT/pytest_$TAG.log 2>&1; rc=$?

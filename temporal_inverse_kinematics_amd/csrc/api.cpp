@@ -137,11 +137,6 @@ static int xnts(int layer) {
     static const int m = [] { const char* e = getenv("TIK_XNTS"); return e ? atoi(e) : 255; }();
     return (m >> layer) & 1;
 }
-// ring depth of the warp-specialized temporal conv (TIK_XWS_S = 3 or 4, default 4)
-static int xws_stages() {
-    static const int v = [] { const char* e = getenv("TIK_XWS_S"); return e && atoi(e) == 3 ? 3 : 4; }();
-    return v;
-}
 // tuning experiments on the xgemm kernels (XArgs::tune), TIK_XTUNE=<bits>; 0 in production
 int xtune() {
     static const int t = getenv("TIK_XTUNE") ? atoi(getenv("TIK_XTUNE")) : 0;
@@ -237,7 +232,6 @@ struct Layer {
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers)
     int xtcon = 0;          // temporal conv on xtconv.hip where packed (TIK_XTC bit mask of layers; off: measured 1-2 % slower than XT128)
-    int xws = 0;            // 128-column temporal convs on the warp-specialized persistent kernel (launch_xgemm_ws; TIK_XWS bit mask of layers; off: measured 3-9 % slower)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
@@ -462,39 +456,12 @@ struct Layer {
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
         t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.nts = xnts(index);
         t.trash = xtrash;
-        const bool ws = xws && xtrash && xt_bn == 128 && xnw != 8 && !(res == RES_IDEN && !t.idn_epi) && tik::xgemm_ws_ok(t);
-        const bool pt = !ws && xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
-        const std::string lab = std::string(ws ? "XW128.L" : xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) +
+        const bool pt = xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
+        const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) +
                                 std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
         p.out(out, (size_t)rout * cout * 4);
-        if (ws) {
-            static const bool wtr = getenv("TIK_X_TRACE") != nullptr;   // debug (-DTIK_XTRACE build): phase sums
-            if (!wtr) {
-                HIP_TRY(tik::launch_xgemm_ws(t, ncu, st, xws_stages()));
-                return TIK_OK;
-            }
-            const int nwg = ncu;
-            unsigned long long* d = nullptr;
-            HIP_TRY(hipMalloc(&d, (size_t)nwg * 16 * 8));
-            HIP_TRY(hipMemset(d, 0, (size_t)nwg * 16 * 8));
-            t.trace = d;
-            HIP_TRY(tik::launch_xgemm_ws(t, ncu, st, xws_stages()));
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<unsigned long long> h((size_t)nwg * 16);
-            HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-            HIP_TRY(hipFree(d));
-            double sm[5] = {0, 0, 0, 0, 0}, sl[5] = {0, 0, 0, 0, 0}, n = 0;
-            for (int w = 0; w < nwg; ++w) {
-                if (!h[16 * w + 5]) continue;
-                n += 1;
-                for (int k = 0; k < 5; ++k) { sm[k] += (double)h[16 * w + k]; sl[k] += (double)h[16 * w + 8 + k]; }
-            }
-            n = std::max(1.0, n);
-            fprintf(stderr, "WSTRACE %-10s wg %4.0f | mfma: bar %8.0f compute %8.0f epi %7.0f lgkm %7.0f total %8.0f | "
-                    "loader: vmwait %8.0f bar %8.0f issue %7.0f prologue %7.0f total %8.0f\n", lab.c_str(), n,
-                    sm[0] / n, sm[1] / n, sm[2] / n, sm[3] / n, sm[4] / n, sl[0] / n, sl[1] / n, sl[2] / n, sl[3] / n, sl[4] / n);
-        } else if (pt) {
+        if (pt) {
             t.trash = xtrash;
             HIP_TRY(tik::launch_xgemm_pt(t, xt_bn, ncu, st));
         } else {
@@ -863,7 +830,6 @@ static void apply_env(tik_model* md) {
             // default: the 64-column temporal convs (6 K steps per tile: the
             // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
             L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
-            if (const char* w = getenv("TIK_XWS")) L.xws = (atoi(w) >> L.index) & 1;
             if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
             if (const char* w = getenv("TIK_XTC")) L.xtcon = (atoi(w) >> L.index) & 1;
             L.xtrash = reinterpret_cast<float*>(md->trash.p);

@@ -54,7 +54,6 @@ struct FkSkinSpArgs {
     const float* transl;             // (B,3): a zero array when the caller has none
     float* verts;                    // (B, 3V)
     int ncu;
-    int nt;                          // nontemporal vertex stores
 };
 hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st);
 

@@ -466,16 +466,7 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
             for (int g = 0; g < 3; ++g)
                 o[g] = fmaf(T[4 * g], cv[b][0], fmaf(T[4 * g + 1], cv[b][1], fmaf(T[4 * g + 2], cv[b][2], T[4 * g + 3]))) +
                        a.transl[bc * 3 + g];
-            if (vok && body < a.B) {
-                float* dst = a.verts + (size_t)body * 3 * a.V + 3 * v;
-                if (a.nt) {
-                    __builtin_nontemporal_store(o[0], dst);
-                    __builtin_nontemporal_store(o[1], dst + 1);
-                    __builtin_nontemporal_store(o[2], dst + 2);
-                } else {
-                    __builtin_memcpy(dst, o, 12);
-                }
-            }
+            if (vok && body < a.B) __builtin_memcpy(a.verts + (size_t)body * 3 * a.V + 3 * v, o, 12);
             __builtin_amdgcn_sched_barrier(0);   // one body's LDS reads in flight at a time (registers)
         }
         if (t + 1 < t1) put((t + 1) & 1);
@@ -495,22 +486,16 @@ hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st) {
     if (a.B <= 0 || a.V <= 0) return hipSuccess;
     if ((a.nz != 4 && a.nz != 8 && a.nz != 16) || !a.ajt || !a.nzw || !a.vposed || !a.verts || !a.transl || a.ldv < 3 * a.V)
         return hipErrorInvalidValue;
-    static const int sbt = getenv("TIK_FK_SBT") && atoi(getenv("TIK_FK_SBT")) == 8 ? 8 : 4;   // experiment
+    constexpr int sbt = 4;   // bodies per tile (8: same time, more VGPRs)
     const int vt = (a.V + 255) / 256, nbt = (a.B + sbt - 1) / sbt;
     // about 4 workgroups per CU, each walking a run of body tiles
     int runs = (4 * (a.ncu > 0 ? a.ncu : 256) + vt - 1) / vt;
     runs = runs < nbt ? runs : nbt;
     (void)hipGetLastError();
     const dim3 grid(vt, runs);
-    if (sbt == 8) {
-        if (a.nz == 4) hipLaunchKernelGGL((fk_skin_sparse_kernel<4, 8>), grid, dim3(256), 0, st, a, runs);
-        else if (a.nz == 8) hipLaunchKernelGGL((fk_skin_sparse_kernel<8, 8>), grid, dim3(256), 0, st, a, runs);
-        else hipLaunchKernelGGL((fk_skin_sparse_kernel<16, 8>), grid, dim3(256), 0, st, a, runs);
-    } else {
-        if (a.nz == 4) hipLaunchKernelGGL((fk_skin_sparse_kernel<4, 4>), grid, dim3(256), 0, st, a, runs);
-        else if (a.nz == 8) hipLaunchKernelGGL((fk_skin_sparse_kernel<8, 4>), grid, dim3(256), 0, st, a, runs);
-        else hipLaunchKernelGGL((fk_skin_sparse_kernel<16, 4>), grid, dim3(256), 0, st, a, runs);
-    }
+    if (a.nz == 4) hipLaunchKernelGGL((fk_skin_sparse_kernel<4, sbt>), grid, dim3(256), 0, st, a, runs);
+    else if (a.nz == 8) hipLaunchKernelGGL((fk_skin_sparse_kernel<8, sbt>), grid, dim3(256), 0, st, a, runs);
+    else hipLaunchKernelGGL((fk_skin_sparse_kernel<16, sbt>), grid, dim3(256), 0, st, a, runs);
     return hipGetLastError();
 }
 

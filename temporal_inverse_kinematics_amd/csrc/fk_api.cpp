@@ -353,10 +353,6 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             s.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
             s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
             s.ncu = fk->ncu;
-            {
-                static const bool nt = getenv("TIK_FK_NT") && getenv("TIK_FK_NT")[0] == '1';   // experiment
-                s.nt = nt ? 1 : 0;
-            }
             // algorithmic: nz joints x 12 entries + the 3x4 vertex transform per (body, vertex);
             // bytes: A_j in, v_posed in, vertices out, the pairs once
             ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),

@@ -84,14 +84,6 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 // epilogue (no identity K steps); bit-identical to launch_xgemm with epi_lds.
 // epi: EPI_BIAS or EPI_SKIN (bn 128, bias = translations (B,3), zeros if none).
 hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int epi = EPI_BIAS);
-// warp-specialized persistent temporal conv (xgemm_ws.hip): 4 loader waves
-// stream the K steps into a 4-stage LDS ring across tiles, 4 MFMA waves compute
-// and store from registers; one 512-thread workgroup per CU (ncu = compute
-// units). Needs Nc % 128 == 0, a.trash, a.bias, no residual-conv rows (a.rx);
-// the identity residual read in the epilogue. Bit-identical to launch_xgemm
-// (bn 128, epi_lds + idn_epi).
-bool xgemm_ws_ok(const XArgs& a);
-hipError_t launch_xgemm_ws(const XArgs& a, int ncu, hipStream_t st, int stages = 4);   // stages: 3 or 4
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
 // out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)

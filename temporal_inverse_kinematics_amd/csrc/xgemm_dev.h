@@ -1,5 +1,5 @@
 // xgemm_dev.h — device pieces shared by the bf16x3 GEMM kernels (xgemm.hip,
-// xgemm_ws.hip): the fp32 -> three-bf16-plane split, the A-image swizzle, the
+// xgraph.hip, xblock.hip, xtconv.hip): the fp32 -> three-bf16-plane split, the A-image swizzle, the
 // epilogue store, and the LDS ring geometry of a tile configuration.
 #pragma once
 #include <hip/hip_runtime.h>

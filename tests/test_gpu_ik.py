@@ -556,25 +556,6 @@ def test_bf16x3_past_2gib_and_config3_batch(N):
     assert np.abs(y[pick[:4]].cpu().numpy() - ref).max() < TOL
 
 
-@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (513, 64)])
-def test_xgemm_ws_bitwise(n, T):
-    """The warp-specialized persistent temporal conv (xgemm_ws.hip: loader
-    waves stream the K steps into a 4-stage ring across tiles, MFMA waves
-    compute and store from registers; opt-in, TIK_XWS) gives poses bit-identical to the
-    per-tile XT128 kernel (the default): same bf16x3 products in the same K order, same
-    (acc + x) + bias epilogue — at the bench size, with partial last tiles,
-    fewer tiles than CUs, and T=65 windows."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    ws = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XWS=255)
-    one = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XWS=0)
-    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 2 * T)).cuda()
-    with torch.no_grad():
-        a = ws(x)["poses"].clone()
-        b = one(x)["poses"]
-    assert torch.isfinite(a).all()
-    assert torch.equal(a, b), float((a - b).abs().max())
-
-
 @pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (2, 9), (1, 1), (5, 31)])
 def test_xblock_whole_blocks_vs_layered(n, T):
     """Blocks 0 and 1 as whole-block kernels (xblock.hip: z kept in LDS, block

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -44,6 +45,7 @@ struct tik_fk {
     bool xpt = true;   // skinning on the persistent xgemm kernel (TIK_FK_PT=0: one workgroup per tile)
     bool skin12 = true;   // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=0: 16)
     int ncu = 256;
+    int gm = -1;       // blend GEMM row-tile group (XArgs::gm); -1 = auto, one group per XCD (TIK_FK_GM)
     int prec = 1;
     // sparse skinning (fk.hip fk_skin_sparse_kernel): per vertex the joints with
     // W > 2^-30 as {joint, weight} pairs, sp_nz per vertex (0: off, TIK_FK_SPARSE=0)
@@ -221,6 +223,7 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
     }
     if (const char* e = getenv("TIK_FK_PT")) fk->xpt = e[0] != '0';
     if (const char* e = getenv("TIK_FK_SKIN12")) fk->skin12 = e[0] != '0';
+    if (const char* e = getenv("TIK_FK_GM")) fk->gm = atoi(e);
     {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
@@ -332,6 +335,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
             g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
             g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
+            // P^T (V3 x 512 bf16x3, ~97 MB) is the large operand: group the row tiles so each XCD
+            // streams it about once (its contiguous run of workgroups covers gm row tiles x all columns)
+            { const int gx = (B + 127) / 128; g.gm = fk->gm >= 0 ? fk->gm : (gx + 7) / 8; }
             // algorithmic: K = 507 live blend-shape columns (486 pose + 20 shape + template);
             // bytes: feat rows in, v_posed out, P^T once
             ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);

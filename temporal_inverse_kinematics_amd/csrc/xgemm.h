@@ -61,6 +61,8 @@ struct XArgs {
     int ksplit;
     int idn_epi;  // with epi_lds: the identity residual added in the epilogue from row-major loads (no K steps)
     int epi_lds;  // EPI_BIAS: stage the C tile through LDS for whole-line row-major stores (else float4 stores from registers)
+    int gm;     // xgemm_kernel tile order: >1 = groups of gm row tiles, columns outer within a group (the B operand
+                // is shared by the gm row tiles running together: for a large B, e.g. the FK blend shapes); else rows outer
     int nw;     // waves per workgroup: 4 (or 0: two 128-row workgroups per CU) or 8 (one 256-row workgroup)
     int tune;   // experiments only (0 = production): 1 skip the A DMA, 2 skip the B DMA, 8 skip the split
     unsigned long long* trace;   // debug (TIK_X_TRACE): 8 s_memtime stamps/sums per workgroup, or null

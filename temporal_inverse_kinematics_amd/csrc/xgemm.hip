@@ -110,8 +110,15 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
         const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
         const int swz = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
-        r0 = (swz / gridDim.y) * RT;
-        ntile = swz % gridDim.y;
+        if (a.gm > 1) {   // groups of gm row tiles; within a group the gm rows of one column tile are adjacent
+            const int gy = gridDim.y, g = swz / (a.gm * gy), w = swz - g * a.gm * gy;
+            const int left = gridDim.x - g * a.gm, ge = left < a.gm ? left : a.gm;
+            r0 = (g * a.gm + w % ge) * RT;
+            ntile = w / ge;
+        } else {
+            r0 = (swz / gridDim.y) * RT;
+            ntile = swz % gridDim.y;
+        }
     }
     const int n0 = ntile * BN;
     const int V = a.V;

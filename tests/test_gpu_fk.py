@@ -169,6 +169,28 @@ def test_fk_sparse_skinning(consts, monkeypatch, nzmax):
     assert torch.equal(v1, vs[36:37])
 
 
+@pytest.mark.parametrize("gm", ["1", "3"])
+def test_fk_blend_tile_order(consts, monkeypatch, gm):
+    """The blend-shape GEMM's grouped tile order (XArgs::gm, TIK_FK_GM; auto =
+    one group of row tiles per XCD) only reorders workgroups: bitwise the same
+    vertices as the row-major order, at a batch whose row tiles do not divide
+    into the groups (1100 bodies = 9 row tiles)."""
+    from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
+    B = 1100
+    pose, betas, expr, transl = _inputs(B, 77)
+    cu = lambda a: torch.from_numpy(a).cuda()
+    outs = []
+    for flag in (None, gm):
+        if flag is None:
+            monkeypatch.delenv("TIK_FK_GM", raising=False)
+        else:
+            monkeypatch.setenv("TIK_FK_GM", flag)
+        m = SMPLX(consts, batch_size=B, precision="bf16x3")
+        outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), cu(transl)))
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+
+
 def _write_smplx_npz(path, c, components=400):
     """The constants in the SMPL-X model-file layout (the keys and shapes of
     SMPLX_{MALE,FEMALE,NEUTRAL}.npz as smplx.body_models.SMPLX reads them):

@@ -26,4 +26,11 @@ bool xtconv_ok(const XTConvArgs& a);
 // one 512-thread workgroup per CU (ncu, even), each a column half of a row range
 hipError_t launch_xtconv(const XTConvArgs& a, int ncu, hipStream_t st);
 
+// the same layer on xtws.hip: weight-stationary (weights in VGPRs), 8-frame
+// tiles whose 10-frame halo is split once per K block for all 3 taps
+// (T % 8 == 0; the same packed weights, wp; the accumulation runs (K block,
+// tap): equal to XT128 up to fp32 rounding of that order)
+bool xtws_ok(const XTConvArgs& a);
+hipError_t launch_xtws(const XTConvArgs& a, int ncu, hipStream_t st);
+
 }  // namespace tik

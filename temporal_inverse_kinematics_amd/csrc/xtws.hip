@@ -1,0 +1,308 @@
+// xtws.hip — tcn conv (3 x 1 over frames, stride 1, 128 -> 128 channels) +
+// folded BN + identity residual + ReLU of an ST-GCN block
+// (st_gcn_aaai18.py:180-189), bf16x3 on MFMA, as one persistent,
+// weight-stationary launch that splits every activation ONCE for all 3 taps.
+//
+// The tiled kernel (XT128) DMAs and splits the conv input three times (once per
+// tap) and re-reads a 24 KB weight stage from L2 for every K step of every
+// tile. Here (the xgraph.hip pattern applied to the temporal conv):
+//   * weights in registers: wave w owns output channels 16w .. 16w + 15, all 3
+//     taps x 128 input channels (144 VGPRs of bf16 planes, loaded once);
+//   * tile = 8 consecutive frames of one window x 17 joints; per 32-channel K
+//     block the 10-frame HALO (frames f0 - 1 .. f0 + 8, zeros outside the
+//     window) is loaded into registers D blocks ahead and split once,
+//     cooperatively, into a double-buffered LDS image of bf16 planes, one
+//     barrier per K block; the three taps read it at frame offsets 0, 1, 2 —
+//     each z element is loaded and split once per tile instead of three times;
+//   * MFMA transposed (A = weights): pixel block j = joints (2j, 2j + 1) x the
+//     tile's 8 frames (9 blocks; the 9th block's second joint is dead), each
+//     lane ends with one pixel and 4 channels, so the epilogue runs on the
+//     accumulators: (acc + x) + bias, ReLU, 16-B stores;
+//   * the identity rows (this wave's 16 channels of the tile's 136 pixels) are
+//     LDS-DMA'd into a per-wave slot a whole tile ahead.
+// Image row R = 10 jj + h (joint jj, halo frame h), 192 B: 3 planes x 4 units
+// of 16 B (8 channels); unit u of joint jj at u ^ 2 (jj & 1): with the 48-dword
+// row pitch, the ds_read_b128 of one (block, tap, plane) is conflict-free in
+// every lane group (lanes of the two joints and the two frame halves land on
+// distinct 4-bank slots).
+// Products as xgemm (bf16x3, six products per K block), fp32 accumulation in
+// the order (K block, tap) — XT128 runs (tap, K block), so the two agree to
+// fp32 rounding of the accumulation order, not bit for bit.
+#include <algorithm>
+#include <type_traits>
+
+#include "xgemm_dev.h"
+#include "xtconv.h"
+
+namespace tik {
+
+namespace xw {
+constexpr int V = 17, F = 8, H = F + 2;       // output frames per tile, halo frames
+constexpr int ROWS = H * V;                   // 170 live image rows
+constexpr int NU = ROWS * 8;                  // 16-B fp32 units of one K block (1360)
+constexpr int NLD = (NU + 511) / 512;         // register loads per lane per K block (3)
+constexpr int PROWB = 192;                    // 3 planes x 32 channels x 2 B
+constexpr int IMG = (ROWS + H) * PROWB;       // + the dead joint 17's rows (read by block 8, never written): 34,560
+constexpr int NB = 9;                         // pixel blocks per tile
+constexpr int IDW = NB * 1024 + 64;           // per-wave identity / output slot: 9 x 16 pixels x 64 B (+ 64: slots 16 banks apart)
+constexpr int NKB = 4;                        // 32-channel K blocks
+constexpr int SMEM = 2 * IMG + 8 * IDW;       // 143,360
+static_assert(SMEM <= 160 * 1024, "LDS");
+}  // namespace xw
+
+__device__ __forceinline__ int xw_unit(int jj, int h, int p, int u) {
+    return (10 * jj + h) * xw::PROWB + ((p * 4 + (u ^ ((jj & 1) << 1))) << 4);
+}
+
+__device__ f32x4 tik_llvm_raw_buffer_load_v4f32_xw(i32x4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+
+typedef __bf16 xwbf16x4 __attribute__((ext_vector_type(4)));
+
+#ifndef XW_XPF
+#define XW_XPF 1   // operand read-ahead (items; 2 spills)
+#endif
+
+#ifdef TIK_XTUNE
+#define XW_OFF(bit) (a.tune & (bit))
+#else
+#define XW_OFF(bit) false
+#endif
+
+template <int D>
+__global__ __launch_bounds__(512, 1) void xtws_kernel(XTConvArgs a) {
+    using namespace xw;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+    auto pimg = [&](int s) __attribute__((always_inline)) { return smem + (s & 1) * IMG; };
+
+    int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned char* const idw = smem + 2 * IMG + wave * IDW;
+    const int T = a.T, tpw = T / F;
+    const int ntiles = a.M / (V * T) * tpw;
+    int t_begin, t_end;
+    {   // persistent: a contiguous run of tiles per workgroup, runs ordered per XCD
+        const int nwg = gridDim.x, bid = blockIdx.x;
+        const int per = nwg >> 3, rem = nwg & 7, x = bid & 7, k = bid >> 3;
+        const int s = x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+        t_begin = (int)((long long)s * ntiles / nwg);
+        t_end = (int)((long long)(s + 1) * ntiles / nwg);
+    }
+    if (t_begin >= t_end) return;
+    const int total = (t_end - t_begin) * NKB;
+    // first output row of tile t (window w, frames f0 .. f0 + 7) and its first frame
+    auto tile_geo = [&](int t, int& row0, int& f0) __attribute__((always_inline)) {
+        const int w = t / tpw;
+        f0 = (t - w * tpw) * F;
+        row0 = (w * T + f0) * V;
+    };
+
+    const i32x4 rZ = buf_rsrc(a.z, (unsigned)((long long)a.M * a.ldz * 4));
+    const i32x4 rXI = buf_rsrc(a.x, (unsigned)((long long)a.M * a.ldx * 4));
+    // ---- the halo rows of global step s (tile t_begin + s / 4, K block s % 4) into registers.
+    // Unit U = 512 i + tid: halo row m = U / 8 (frame f0 - 1 + m / 17, joint m % 17), channels 4 (U % 8) ..
+    // Every lane issues NLD loads per step (out-of-range offsets read zeros): no branch, exact vmcnt
+    f32x4 rb[D][NLD];
+    auto load_unit = [&](int s, f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
+        const int t = t_begin + s / NKB, kb = s - (s / NKB) * NKB;
+        int row0, f0;
+        tile_geo(t, row0, f0);
+        const bool live = s < total;
+        const int U = 512 * i + tid, m = U >> 3, u = U & 7;
+        const int fh = f0 - 1 + m / V;
+        const bool ok = live && U < NU && fh >= 0 && fh < T && !XW_OFF(1);
+        const unsigned off = ok ? (unsigned)((long long)(row0 - V + m) * a.ldz * 4 + kb * 128 + u * 16) : DMA_OOB;
+        r[i] = tik_llvm_raw_buffer_load_v4f32_xw(rZ, (int)off, 0, 0);
+    };
+    auto load = [&](int s, f32x4 (&r)[NLD]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) load_unit(s, r, i);
+    };
+    // ---- split registers r (step s) into planes image (s & 1)
+    auto split_unit = [&](int s, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
+        unsigned char* P = pimg(s);
+        const int U = 512 * i + tid;
+        if (i + 1 < NLD || U < NU) {
+            const int m = U >> 3, u = U & 7;
+            const int h = m / V, jj = m - h * V;
+            xwbf16x4 p0, p1, p2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
+                const float x = r[i][e];
+                const __bf16 b0 = (__bf16)x;
+                const float r1 = x - (float)b0;
+                const __bf16 b1 = (__bf16)r1;
+                p0[e] = b0;
+                p1[e] = b1;
+                p2[e] = (__bf16)(r1 - (float)b1);
+            }
+            const int hb = (u & 1) * 8;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 0, u >> 1) + hb) = p0;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 1, u >> 1) + hb) = p1;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 2, u >> 1) + hb) = p2;
+        }
+    };
+    auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) split_unit(s, r, i);
+    };
+    // ---- identity rows of tile t (this wave's 16 channels) into the wave's LDS slot:
+    // instruction j, lane l: pixel l / 4 of block j, 16-B piece l % 4 -> slot + 64 (16 j + l / 4) + 16 (l % 4)
+    auto dma_ident = [&](int t) __attribute__((always_inline)) {
+        int row0, f0;
+        tile_geo(t, row0, f0);
+        const bool live = t < t_end;
+        const int pp = lane >> 2, c = lane & 3;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int jj = 2 * j + (pp >> 3), fi = pp & 7;
+            const bool ok = live && jj < V && !XW_OFF(1);
+            const unsigned off = ok ? (unsigned)((long long)(row0 + fi * V + jj) * a.ldx * 4 + (16 * wave + 4 * c) * 4) : DMA_OOB;
+            dma16(rXI, idw + j * 1024, off, 0);
+        }
+    };
+
+    // weights: [cg][tap * 4 + kb][plane][lane][8] (xblock_pack_weights), this wave's cg = wave
+    xbf16x8 w[3 * NKB][3];
+#pragma unroll
+    for (int k = 0; k < 3 * NKB; ++k)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            w[k][p] = *reinterpret_cast<const xbf16x8*>(a.wp + ((((size_t)wave * 3 * NKB + k) * 3 + p) * 64 + lane) * 8);
+    const int g = lane >> 4, px = lane & 15;
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(a.bias + 16 * wave + 4 * g);
+
+    // prologue: step 0 -> planes[0]; steps 1 .. D into registers
+    load(0, rb[0]);
+    split(0, rb[0]);
+#pragma unroll
+    for (int d = 1; d <= D; ++d) load(d, rb[d % D]);
+
+    f32x4 acc[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // one K block; KB compile-time so the weights and the prefetch registers are statically indexed
+    auto step = [&](int s, int t, auto KBc) __attribute__((always_inline)) {
+        constexpr int kb = decltype(KBc)::value;
+        constexpr int nb = (kb + 1) % D;   // registers holding step s+1 (s % D == kb % D: 4 % D == 0)
+        asm volatile("" : "+v"(tid), "+v"(lane));   // lane-derived addresses: not hoisted across steps
+        // every wave's split(s) landed; every wave done with step s-1's image (the one split(s+1) writes)
+        lds_barrier();
+        if constexpr (kb == 0) {
+            // this tile's identity rows into the wave's slot (every wave is done with the
+            // previous tile's outputs there: the barrier above)
+            __builtin_amdgcn_sched_barrier(0);
+            dma_ident(t);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const unsigned char* P = pimg(s);
+        const int jb = px >> 3, fb = px & 7;
+        // operand ring over the 27 (block, tap) items: item n + 1's planes are read while item n's MFMAs run
+        constexpr int NI = NB * 3, XPF = XW_XPF;
+        xbf16x8 xr[XPF + 1][3];
+        auto rd = [&](int n, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
+            const int j = n / 3, tap = n - 3 * (n / 3);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(P + xw_unit(2 * j + jb, fb + tap, p, g));
+        };
+        auto mfma_n = [&](int n) __attribute__((always_inline)) {
+            if (n + XPF < NI) rd(n + XPF, xr[(n + XPF) % (XPF + 1)]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (XW_OFF(4)) return;
+            const int j = n / 3, tap = n - 3 * (n / 3);
+            const xbf16x8(&x)[3] = xr[n % (XPF + 1)];
+            const xbf16x8(&wk)[3] = w[tap * NKB + kb];
+            // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgemm's product order
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[2], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[1], x[1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[2], x[0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[1], x[0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[0], acc[j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+#pragma unroll
+        for (int n = 0; n < XPF; ++n) rd(n, xr[n]);
+        // the next K block's split, one 16-B unit at a time, spread over this block's
+        // MFMA items (the two waves of a SIMD leave the barrier together: a split in
+        // one piece would idle the MFMA pipe of both), each unit's register slot
+        // reloaded right after (past the run: zeros, never read)
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+            mfma_n(n);
+            if (n % 8 == 3 && n / 8 < NLD) {
+                const int i = n / 8;
+                if (!XW_OFF(2)) split_unit(s + 1, rb[nb], i);
+                load_unit(s + 1 + D, rb[nb], i);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (kb == NKB - 1) {
+            // ---- epilogue: (acc + x) + bias, ReLU. The identity DMA of this tile was issued
+            // before the NKB * NLD register loads of its K blocks: at most that many may stay in flight
+            wait_vm<NKB * NLD>();
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                f32x4* sl = reinterpret_cast<f32x4*>(idw + (16 * j + px) * 64 + g * 16);
+                f32x4 v = acc[j] + *sl;
+                v += bv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                *sl = v;   // the output replaces the identity in the slot
+                acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            // whole output rows from the 8 slots: 32 lanes x 16 B = one 512-B row
+            lds_barrier();
+            int row0, f0;
+            tile_geo(t, row0, f0);
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+                const int q = tid + 512 * i, pix = q >> 5, cu = q & 31;
+                const int j = pix >> 4, pp = pix & 15, jj = 2 * j + (pp >> 3);
+                const f32x4 v = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + (cu >> 2) * IDW + pix * 64 + (cu & 3) * 16);
+                float* o = jj < V ? a.out + (size_t)(row0 + (pp & 7) * V + jj) * a.ldo + cu * 4 : a.trash + (tid & 255) * 4;
+                if (!XW_OFF(8)) xst4(o, v, a.nts);
+            }
+        }
+    };
+    for (int t = t_begin; t < t_end; ++t) {
+        const int s0 = (t - t_begin) * NKB;
+        step(s0, t, std::integral_constant<int, 0>{});
+        step(s0 + 1, t, std::integral_constant<int, 1>{});
+        step(s0 + 2, t, std::integral_constant<int, 2>{});
+        step(s0 + 3, t, std::integral_constant<int, 3>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool xtws_ok(const XTConvArgs& a) {
+    return a.T > 0 && a.T % xw::F == 0 && a.ldz % 4 == 0 && a.ldz >= 128 && a.ldx % 4 == 0 && a.ldx >= 128 &&
+           a.ldo % 4 == 0 && a.ldo >= 128;
+}
+
+hipError_t launch_xtws(const XTConvArgs& a, int ncu, hipStream_t st) {
+    if (a.M <= 0) return hipSuccess;
+    if (!xtws_ok(a) || !a.z || !a.x || !a.wp || !a.bias || !a.out || !a.trash || ncu <= 0 || a.M % (17 * a.T) != 0)
+        return hipErrorInvalidValue;
+    // the buffer offsets are 32-bit: launches of whole windows, < 2 GiB of conv input and identity rows each
+    const long long win = 17LL * a.T, win_bytes = win * std::max(a.ldz, a.ldx) * 4;
+    if (win_bytes >= (1LL << 31)) return hipErrorInvalidValue;
+    const long long wper = std::max(1LL, ((1LL << 31) - 1) / win_bytes);
+    const long long rows_per = wper * win;
+    (void)hipGetLastError();
+    for (long long r0 = 0; r0 < a.M; r0 += rows_per) {
+        XTConvArgs c = a;
+        c.M = (int)std::min(rows_per, (long long)a.M - r0);
+        c.z = a.z + (size_t)r0 * a.ldz;
+        c.x = a.x + (size_t)r0 * a.ldx;
+        c.out = a.out + (size_t)r0 * a.ldo;
+        const int ntiles = (int)(c.M / win) * (a.T / xw::F);
+        hipLaunchKernelGGL((xtws_kernel<1>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace tik

@@ -620,6 +620,35 @@ def test_xtconv_vs_tiled(n, T):
     assert torch.equal(a, b), float((a - b).abs().max())
 
 
+@pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9)])
+def test_xtws_vs_tiled_and_oracle(n, T):
+    """The temporal conv of the 128-channel stride-1 blocks (L3, L4) as the
+    weight-stationary halo kernel (xtws.hip, TIK_XTWS: weights in VGPRs, the
+    10-frame halo of an 8-frame tile split once for all 3 taps) against the
+    tiled XT128 kernel (TIK_XTWS=0) and the oracle. Its accumulation runs (K
+    block, tap) where XT128 runs (tap, K block), so the check is fp32-rounding
+    close, not bitwise: at the bench size, one tile per window (both halo
+    frames zero), three tiles per window, and T=9 (L3 has 5 frames: not a
+    multiple of 8, the tiled kernel runs)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    xw = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTWS=255)
+    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTWS=0)
+    xh = syn.synthetic_windows(n, T, seed=n * 7 + T)
+    x = torch.from_numpy(xh).cuda()
+    with torch.no_grad():
+        a = xw(x)["poses"].clone()
+        b = tl(x)["poses"]
+        fa = xw.backbone_features(x)
+        fb = tl.backbone_features(x)
+    assert torch.isfinite(a).all()
+    assert float((a - b).abs().max()) < 2e-5
+    assert float((fa - fb).abs().max()) <= 2e-5 * max(1.0, float(fb.abs().max()))
+    sd = {k: v.detach().cpu().numpy() for k, v in xw.state_dict().items()}
+    idx = [0, n - 1]
+    ref = orc.pose_regressor(xh[idx], sd)["poses"]
+    assert np.abs(a[idx].cpu().numpy() - ref).max() < TOL
+
+
 def test_run_test_end_to_end_and_cli(tmp_path):
     """inference.run_test (`/root/reference/inference.py:110-145`) end to end on
     the reference's shipped moveai sample (data/sample_3d_poses/

@@ -78,6 +78,8 @@ def kernel_symbol(label, precision):
         return "tik::xgraph_kernel"   # <K blocks, passes>: the label does not say which (any instantiation)
     if label == "XTC":
         return "tik::xtconv_kernel"
+    if label == "XTW":
+        return "tik::xtws_kernel"
     p = PREC_CODE[precision]
     nb_graph = 2 if p == 0 else 1
     cg = {"G272x64": f"272, 64, 1, 4, 1, 17, {p}, {nb_graph}", "T128x128": f"128, 128, 2, 2, 0, 0, {p}, 2",

@@ -231,7 +231,7 @@ struct Layer {
     int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
     int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
     int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers)
-    int xtwson = 0;         // temporal conv on xtws.hip where packed (TIK_XTWS bit mask of layers)
+    int xtwson = 1;         // temporal conv on xtws.hip where packed (TIK_XTWS bit mask of layers; 0 = XT128)
     int xtcon = 0;          // temporal conv on xtconv.hip where packed (TIK_XTC bit mask of layers; off: measured 1-2 % slower than XT128)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
@@ -425,7 +425,7 @@ struct Layer {
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
-        if (xtwson && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0) {
+        if (xtwson && !xtcon && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0) {
             tik::XTConvArgs c{};
             c.M = (int)rout; c.T = tin; c.z = z; c.ldz = cout; c.x = x; c.ldx = ld; c.wp = xtw.p; c.bias = biasT.p;
             c.out = out; c.ldo = cout; c.nts = xnts(index); c.trash = xtrash; c.tune = xtune();

@@ -23,9 +23,10 @@
 //     writes its outputs over them and all waves then store whole 512-B rows;
 //   * the next K block's split runs one 16-B unit at a time between the MFMA
 //     items (the waves leave each barrier together).
-// Measured (L3/L4, 1024 x 64 windows): 0.288 ms vs 0.301 for XT128 on the same
-// box; components (-DTIK_XTUNE): no MFMAs 0.210, MFMAs + operand reads only
-// 0.193 (the MFMA roof is 0.138) — opt-in (TIK_XTWS), not the default.
+// Measured (L3/L4, 1024 x 64 windows, same box): 0.265 ms vs 0.281-0.291 for
+// XT128; components (-DTIK_XTUNE, before the row staging and the priority): no
+// MFMAs 0.210, MFMAs + operand reads only 0.193 (the MFMA roof is 0.138).
+// The default for L3/L4 (TIK_XTWS=0 restores XT128).
 // Image row R = 10 jj + h (joint jj, halo frame h), 192 B: 3 planes x 4 units
 // of 16 B (8 channels); unit u of joint jj at u ^ 2 (jj & 1): with the 48-dword
 // row pitch, the ds_read_b128 of one (block, tap, plane) is conflict-free in
@@ -294,6 +295,10 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             }
         }
     };
+    // static priority for the younger half of the workgroup (waves 4-7 lose VALU arbitration
+    // to their older SIMD partners on every segment: MI355X_MICROARCH.md, two waves per SIMD):
+    // 0.265 vs 0.272 ms on L3. 8 waves only (the condition must be wave-uniform: readfirstlane)
+    if (NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int t = t_begin; t < t_end; ++t) {
         const int s0 = (t - t_begin) * NKB;
         step(s0, t, std::integral_constant<int, 0>{});

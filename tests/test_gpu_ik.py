@@ -471,7 +471,7 @@ def test_xgemm_epilogue_variants():
     registers (0) the compiler contracts layer 0's residual-conv terms into
     FMAs differently: equal to fp32 rounding."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    ms = [_model_with_env("bf16x3", TIK_SPLIT=0, TIK_XEPI=e) for e in (0, 1, 2)]
+    ms = [_model_with_env("bf16x3", TIK_SPLIT=0, TIK_XEPI=e, TIK_XTWS=0) for e in (0, 1, 2)]
     for n in (1024, 37):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 5)).cuda()
         with torch.no_grad():
@@ -508,8 +508,8 @@ def test_xgemm_persistent_bitwise(n, T):
     differently by the two kernels, so both sides run it on the persistent
     kernel: TIK_XPT=1 vs 255.)"""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    pt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=255)
-    one = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=1)
+    pt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=255, TIK_XTWS=0)
+    one = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=1, TIK_XTWS=0)
     x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + T)).cuda()
     with torch.no_grad():
         a = pt(x)["poses"].clone()
@@ -605,13 +605,13 @@ def test_xtconv_vs_tiled(n, T):
     """The temporal conv of the 128-channel stride-1 blocks as the
     resident-weight persistent kernel (xtconv.hip: weights in LDS, activations
     straight into registers; opt-in, TIK_XTC) against the tiled XT128 kernel
-    (TIK_XTC=0): the same bf16x3 products in the same K order and the same
+    (TIK_XTC=0, TIK_XTWS=0): the same bf16x3 products in the same K order and the same
     (acc + x) + bias epilogue, so the poses are bit-identical — at the bench
     size, partial last row blocks, short windows (taps at both edges), single
     frames and T=65."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     xt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=255)
-    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=0)
+    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=0, TIK_XTWS=0)
     x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n * 3 + T)).cuda()
     with torch.no_grad():
         a = xt(x)["poses"].clone()
@@ -623,7 +623,7 @@ def test_xtconv_vs_tiled(n, T):
 @pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9)])
 def test_xtws_vs_tiled_and_oracle(n, T):
     """The temporal conv of the 128-channel stride-1 blocks (L3, L4) as the
-    weight-stationary halo kernel (xtws.hip, TIK_XTWS: weights in VGPRs, the
+    weight-stationary halo kernel (xtws.hip, the default: weights in VGPRs, the
     10-frame halo of an 8-frame tile split once for all 3 taps) against the
     tiled XT128 kernel (TIK_XTWS=0) and the oracle. Its accumulation runs (K
     block, tap) where XT128 runs (tap, K block), so the check is fp32-rounding

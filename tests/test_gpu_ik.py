@@ -620,7 +620,7 @@ def test_xtconv_vs_tiled(n, T):
     assert torch.equal(a, b), float((a - b).abs().max())
 
 
-@pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9)])
+@pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9), (1, 16), (7, 128), (257, 32), (33, 96)])
 def test_xtws_vs_tiled_and_oracle(n, T):
     """The temporal conv of the 128-channel stride-1 blocks (L3, L4) as the
     weight-stationary halo kernel (xtws.hip, the default: weights in VGPRs, the
@@ -628,8 +628,10 @@ def test_xtws_vs_tiled_and_oracle(n, T):
     tiled XT128 kernel (TIK_XTWS=0) and the oracle. Its accumulation runs (K
     block, tap) where XT128 runs (tap, K block), so the check is fp32-rounding
     close, not bitwise: at the bench size, one tile per window (both halo
-    frames zero), three tiles per window, and T=9 (L3 has 5 frames: not a
-    multiple of 8, the tiled kernel runs)."""
+    frames zero), three tiles per window, T=9 (L3 has 5 frames: not a
+    multiple of 8, the tiled kernel runs), a single tile (grid of one
+    workgroup), 8 tiles per window, and batches whose tiles do not divide
+    evenly over the workgroups."""
     from temporal_inverse_kinematics_amd import synthetic as syn
     xw = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTWS=255)
     tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTWS=0)

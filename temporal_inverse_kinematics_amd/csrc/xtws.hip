@@ -71,6 +71,13 @@ __device__ f32x4 tik_llvm_raw_buffer_load_v4f32_xw(i32x4 rsrc, int voffset, int 
 
 typedef __bf16 xwbf16x4 __attribute__((ext_vector_type(4)));
 
+#ifndef XW_D
+#define XW_D 1     // K blocks of register prefetch
+#endif
+#ifndef XW_SPLIT_AT
+#define XW_SPLIT_AT 0   // split unit i after item: 0 = (2 i + 1) NI / (2 NLD) (midpoints), 1 = i NI / NLD + 1
+#endif
+
 #ifndef XW_XPF
 #define XW_XPF 1   // operand read-ahead (items; 2 spills at 8 waves)
 #endif
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             mfma_n(n);
 #pragma unroll
             for (int i = 0; i < NLD; ++i)
-                if (n == ((2 * i + 1) * NI) / (2 * NLD)) {
+                if (n == (XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD))) {
                     if (!XW_OFF(2)) split_unit(s + 1, rb[nb], i);
                     load_unit(s + 1 + D, rb[nb], i);
                     __builtin_amdgcn_sched_barrier(0);
@@ -333,7 +340,7 @@ hipError_t launch_xtws(const XTConvArgs& a, int ncu, hipStream_t st) {
         const int ntiles = (int)(c.M / win) * (a.T / xw::F);
         // 8 waves (two per SIMD, 16 channels each); 4 waves of 32 channels (one per SIMD, the weights
         // through AGPRs: v_accvgpr_read before every MFMA group) measured 0.364 vs 0.288 ms
-        hipLaunchKernelGGL((xtws_kernel<1, 8>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
+        hipLaunchKernelGGL((xtws_kernel<XW_D, 8>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

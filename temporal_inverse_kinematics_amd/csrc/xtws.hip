@@ -78,6 +78,10 @@ typedef __bf16 xwbf16x4 __attribute__((ext_vector_type(4)));
 #define XW_SPLIT_AT 0   // split unit i after item: 0 = (2 i + 1) NI / (2 NLD) (midpoints), 1 = i NI / NLD + 1
 #endif
 
+#ifndef XW_EPIBAR
+#define XW_EPIBAR 1   // no barrier at a tile's first K block (the epilogue's serves), identity DMA at K block 1 (0: both at K block 0; 0.5 % slower)
+#endif
+
 #ifndef XW_XPF
 #define XW_XPF 1   // operand read-ahead (items; 2 spills at 8 waves)
 #endif
@@ -217,8 +221,16 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         constexpr int nb = (kb + 1) % D;   // registers holding step s+1 (s % D == kb % D: 4 % D == 0)
         asm volatile("" : "+v"(tid), "+v"(lane));   // lane-derived addresses: not hoisted across steps
         // every wave's split(s) landed; every wave done with step s-1's image (the one split(s+1) writes)
+#if XW_EPIBAR
+        // at a tile's first K block the previous tile's epilogue barrier (after this image's
+        // split and the last reads of the other one) already holds, except at the run's start
+        if (kb != 0 || t == t_begin) lds_barrier();
+        constexpr int KDMA = 1;
+#else
         lds_barrier();
-        if constexpr (kb == 0) {
+        constexpr int KDMA = 0;
+#endif
+        if constexpr (kb == KDMA) {
             // this tile's identity rows into the wave's slot (every wave is done with the
             // previous tile's outputs there: the barrier above)
             __builtin_amdgcn_sched_barrier(0);
@@ -273,8 +285,8 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         }
         if constexpr (kb == NKB - 1) {
             // ---- epilogue: (acc + x) + bias, ReLU. The identity DMA of this tile was issued
-            // before the NKB * NLD register loads of its K blocks: at most that many may stay in flight
-            wait_vm<NKB * NLD>();
+            // before the register loads of its K blocks KDMA .. 3: at most that many may stay in flight
+            wait_vm<(NKB - KDMA) * NLD>();
 #pragma unroll
             for (int j = 0; j < NB; ++j)
 #pragma unroll

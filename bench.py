@@ -30,43 +30,20 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 / f16 MFMA: 1024 FLOP/clk/SIMD x 4 
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 # MFMA products per fp32 product, and the dense peak of the MFMA that executes them
 ARITH = {"bf16x3": (6, BF16_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x32_bf16"),
-         "f16x3": (3, BF16_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x32_f16"),
          "fp32": (1, FP32_MFMA_PEAK_TFLOPS, "v_mfma_f32_16x16x4_f32")}
 DTYPE = {"bf16x3": "f32 via bf16x3 (x = 3 bf16 planes, 6 MFMA products, fp32 accumulate; fp32 exponent range)",
-         "f16x3": "f32 via f16x3 (3 MFMA products; f16 range, narrower than fp32)",
          "fp32": "f32 (exact fp32 MFMA)"}
-PREC_CODE = {"fp32": 0, "f16x3": 1, "bf16x3": 2}
-
-# profiler label prefix (csrc/api.cpp ProfScope) -> kernel symbol in rocprofv3 output
-KERNEL_SYMBOLS = {
-    "G3_272x128": "tik::cgemm3_kernel<272, 128, 1, 8, 1, 17, 3, 0>",
-    "G3_272x64": "tik::cgemm3_kernel<272, 64, 1, 4, 1, 17, 1, 0>",
-    "T3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 0>",
-    "T3_128x64": "tik::tgemm_kernel<128, 64, 4, 2, 3, 0>",
-    "TG3_128x128": "tik::tgemm_kernel<128, 128, 2, 4, 3, 7>",
-    "TW_128": "tik::tgw_kernel<3, 2>",
-    "GP_128": "tik::gpw_kernel<64, 128, 4, 4, 1>",
-    "GP_256": "tik::gpw_kernel<128, 256, 3, 8, 2>",
-    "TH_128x128": "tik::tconv_halo_kernel<128, 2, 4>",
-    "TH_128x64": "tik::tconv_halo_kernel<64, 4, 2>",
-    "H3_64x64": "tik::cgemm3_kernel<64, 64, 2, 2, 0, 0, 3, 0>",
-    "G0_raw": "tik::gcn0_kernel<1>",
-    "B3_64": "tik::stblock_kernel<64, 64, 16, false>",
-    "B0_64": "tik::stblock_kernel<64, 64, 16, true>",
-}
+PREC_CODE = {"fp32": 0, "bf16x3": 2}
 
 
 def kernel_symbol(label, precision):
-    """rocprofv3 symbol of the launch behind a profiler label (register-staged
-    cgemm.hip tiles are templated on the precision code)."""
-    if label in KERNEL_SYMBOLS:
-        return KERNEL_SYMBOLS[label]
+    """rocprofv3 symbol of the launch behind a profiler label (csrc/api.cpp
+    ProfScope; register-staged cgemm.hip tiles are templated on the precision code)."""
     if label == "G0f_raw":
-        return "tik::gcn0_kernel<1, true>"
+        return "tik::gcn0_kernel<1>"
     if label[:2] in ("XT", "XG", "XH") and label[2:] in ("64", "128"):
-        # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), waves per workgroup (TIK_XNW)>
-        nw = 8 if os.environ.get("TIK_XNW", "") == "8" else 4
-        return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, {nw}, {'true' if label[1] == 'H' else 'false'}>"
+        # xgemm.hip: <BN, EPI_BIAS (0) | EPI_GRAPH (1), 4 waves per workgroup, split-K>
+        return f"tik::xgemm_kernel<{label[2:]}, {1 if label[1] == 'G' else 0}, 4, {'true' if label[1] == 'H' else 'false'}>"
     if label in ("XB0", "XB1"):
         return f"tik::xblock_kernel<{'true' if label == 'XB0' else 'false'}>"
     if label[:2] == "XP" and label[2:] in ("64", "128"):
@@ -76,8 +53,6 @@ def kernel_symbol(label, precision):
         return "tik::xgemm_splitk_reduce_kernel"
     if label == "XGW":
         return "tik::xgraph_kernel"   # <K blocks, passes>: the label does not say which (any instantiation)
-    if label == "XTC":
-        return "tik::xtconv_kernel"
     if label == "XTW":
         return "tik::xtws_kernel"
     p = PREC_CODE[precision]
@@ -88,33 +63,44 @@ def kernel_symbol(label, precision):
     return f"tik::cgemm_kernel<{cg[label]}>" if label in cg else None
 
 
-def newest_profile(pattern):
-    """The newest profiles/`pattern` by the rNN_vMM tag in its name (file
-    mtimes are checkout times, not measurement order), or None."""
+def tree_profile(pattern):
+    """The profiles/`pattern` summary of THIS source tree: the PMC summaries
+    carry the sha256 digest of the library sources they were measured on
+    (scripts/pmc_traffic.py, pmc_mfma.py; _build.source_digest), and only a
+    summary whose digest equals the benchmarked tree's is used (the last by
+    name when several match). Returns (path or None, reason)."""
     import glob
-    import re
 
-    def key(p):
-        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(p))
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-    cands = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), key=key)
-    return cands[-1] if cands else None
+    from temporal_inverse_kinematics_amd._build import source_digest
+    digest = source_digest()
+    hits = []
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", pattern))):
+        try:
+            if json.load(open(p)).get("source_digest") == digest:
+                hits.append(p)
+        except (OSError, ValueError):
+            continue
+    if not hits:
+        return None, f"no profiles/{pattern} was measured on this source tree (digest {digest})"
+    return hits[-1], f"measured on this source tree (digest {digest})"
 
 
 def _pmc_value(path, label, pattern, field, precision):
     """`field` of the kernel behind `label` in a PMC summary (scripts/pmc_traffic.py
-    or pmc_mfma.py output; default: the newest profiles/`pattern`), or None."""
+    or pmc_mfma.py output; default: the profiles/`pattern` summary of this
+    source tree, tree_profile). Returns (value or None, source path or None, note)."""
+    note = "explicit path"
     if path is None:
-        path = newest_profile(pattern)
+        path, note = tree_profile(pattern)
     if not path or not os.path.exists(path):
-        return None, None
+        return None, None, note
     sym = kernel_symbol(label, precision)
     kern = json.load(open(path)).get("kernels", {})
     for k, v in kern.items():
         name = k.replace("void ", "").strip()
         if sym and (name == sym or ("<" not in sym and name.startswith(sym + "<"))):
-            return v.get(field), os.path.relpath(path, REPO)
-    return None, os.path.relpath(path, REPO)
+            return v.get(field), os.path.relpath(path, REPO), note
+    return None, os.path.relpath(path, REPO), note + f"; no entry for {sym}"
 
 
 def _pmc_traffic(path, label, precision):
@@ -137,45 +123,89 @@ def _cpu_model():
     return "unknown"
 
 
-def _cpu_baseline(T: int, seconds: float = 12.0):
-    """The reference forward restated with the torch CPU ops the reference runs
-    (oracle/stgcn.py pose_regressor_torch, pinned to the reference's fixtures),
-    fp32, eval, on a bounded sample, in batches of 64 windows (the reference's
-    inference batch, inference.py:43). Thread count: 16, 32, 64, 128 and 256
-    (those the process may run on, sched_getaffinity) probed on one batch each;
-    the fastest is used and reported with every probe's rate."""
+def _one_socket_physical_cores():
+    """CPUs this process may run on, restricted to the socket of the first one
+    and to one hardware thread per physical core (sysfs topology)."""
+    allowed = sorted(os.sched_getaffinity(0))
+
+    def rd(c, f):
+        try:
+            return open(f"/sys/devices/system/cpu/cpu{c}/topology/{f}").read().strip()
+        except OSError:
+            return None
+    pkg0 = rd(allowed[0], "physical_package_id")
+    seen, cores = set(), []
+    for c in allowed:
+        if rd(c, "physical_package_id") != pkg0:
+            continue
+        key = rd(c, "core_id")
+        if key in seen:
+            continue
+        seen.add(key)
+        cores.append(c)
+    return cores or allowed
+
+
+def _cgroup_cpus():
+    """The CPU share of this container's cgroup (cpu.max quota / period), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_child(T: int, seconds: float):
+    """The CPU baseline itself, in a child process (bench.py --cpu-child): pinned
+    to the physical cores of one socket BEFORE torch is imported, so the intra-op
+    threads never spread over two sockets or SMT siblings."""
+    cores = _one_socket_physical_cores()
+    os.sched_setaffinity(0, cores)
     import numpy as np
     import torch
 
     from oracle import stgcn as orc
     from temporal_inverse_kinematics_amd import synthetic as syn
     sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
-    nb = 64
+    nb = 64   # the reference's inference batch (inference.py:43)
     x = syn.synthetic_windows(nb, T, seed=7)
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cands = sorted({n for n in (16, 32, 64, 128, 256) if n <= avail} | {min(16, avail)})
-    best, rate, probes = cands[0], 0.0, {}
+    quota = _cgroup_cpus()
+    cap = len(cores) if quota is None else max(1, min(len(cores), int(quota)))
+    cands = [n for n in (8, 16, 32, 64) if n <= cap] or [cap]
+    probes = {}
     for n in cands:
         torch.set_num_threads(n)
-        orc.pose_regressor_torch(x[:4], sd)
+        orc.pose_regressor_torch(x, sd)   # warm-up batch at this thread count
         t0 = time.perf_counter()
         orc.pose_regressor_torch(x, sd)
-        r = nb / (time.perf_counter() - t0)
-        probes[str(n)] = round(r, 1)
-        if r > rate:
-            best, rate = n, r
+        probes[str(n)] = round(nb / (time.perf_counter() - t0), 1)
+    best = int(max(probes, key=lambda k: probes[k]))
     torch.set_num_threads(best)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        orc.pose_regressor_torch(x, sd)
-        done += nb
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 1), "unit": "IK frames/s", "cores": int(best), "kind": "port",
-            "cpu_model": _cpu_model(), "visible_cpus": os.cpu_count(), "affinity_cpus": avail,
-            "threads_probed": probes,
-            "sample": f"{done} windows (T={T}, batches of {nb}) of the reference forward restated in torch CPU ops "
-                      f"(oracle/stgcn.py pose_regressor_torch, fp32 eval, pinned to the reference's fixtures) "
-                      f"in {dt:.1f}s on {best} threads"}
+    rates, done_all = [], 0
+    for _ in range(3):   # three windows; the median is the value
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 3:
+            orc.pose_regressor_torch(x, sd)
+            done += nb
+        rates.append(done / (time.perf_counter() - t0))
+        done_all += done
+    return {"value": round(float(np.median(rates)), 1), "unit": "IK frames/s", "cores": best, "kind": "port",
+            "cpu_model": _cpu_model(), "pinned_cpus": len(cores), "cgroup_cpus": quota,
+            "visible_cpus": os.cpu_count(), "threads_probed": probes, "windows_rates": [round(r, 1) for r in rates],
+            "sample": f"{done_all} windows (T={T}, batches of {nb}) of the reference forward restated in torch CPU ops "
+                      f"(oracle/stgcn.py pose_regressor_torch, fp32 eval, pinned to the reference's fixtures), "
+                      f"{best} threads pinned to {len(cores)} physical cores of one socket; median of 3 windows "
+                      f"of {seconds / 3:.1f} s"}
+
+
+def _cpu_baseline(T: int, seconds: float = 12.0):
+    """CPU baseline (report only) in a child process, see _cpu_child."""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", "--T", str(T),
+                        "--cpu-seconds", str(seconds)], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"value": None, "error": r.stderr[-500:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def main():
@@ -187,9 +217,9 @@ def main():
     ap.add_argument("--T", type=int, default=64, help="frames per window")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "f16x3"],
-                    help="GEMM arithmetic: bf16x3 (default; fp32 range, 6 bf16 MFMA products), exact fp32 "
-                         "MFMA, or the narrower-range f16x3 split")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"],
+                    help="GEMM arithmetic: bf16x3 (default; fp32 range, 6 bf16 MFMA products) or exact fp32 MFMA")
+    ap.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-compare", action="store_true", help="skip the other-precision comparison runs")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the config #4 (fk) and #5 (online) measurements appended at N=1")
@@ -200,6 +230,9 @@ def main():
     ap.add_argument("--pmc-mfma", default=None,
                     help="PMC MFMA-busy summary (scripts/pmc_mfma.py); default: newest profiles/*pmc_mfma*.json")
     args = ap.parse_args()
+    if args.cpu_child:
+        print(json.dumps(_cpu_child(args.T, args.cpu_seconds)))
+        return
 
     import numpy as np
     import torch
@@ -314,7 +347,7 @@ def main():
         # the other arithmetics on the same inputs: time + max |difference| of the poses
         with torch.no_grad():
             y_main = reg(x)["poses"].clone()
-            for alt in [p for p in ("fp32", "f16x3", "bf16x3") if p != args.precision]:
+            for alt in [p for p in ("fp32", "bf16x3") if p != args.precision]:
                 reg.tik_precision = alt
                 y_alt = reg(x)["poses"]
                 for _ in range(2):
@@ -356,8 +389,8 @@ def main():
             bound, achieved, peak, unit = "mfma", tflops, xpeak / nprod, "TFLOP/s"
             basis = (f"{instr} dense peak {xpeak} TF / {nprod} MFMA products per fp32 product = {xpeak / nprod:.1f} "
                      f"fp32-equivalent TF; achieved = algorithmic fp32 FLOPs (SURVEY.md §8(d)) / HIP-event launch time")
-        traffic, traffic_src = _pmc_traffic(args.pmc_traffic, dom, args.precision)
-        mfma_busy, mfma_src = _pmc_mfma(args.pmc_mfma, dom, args.precision)
+        traffic, traffic_src, traffic_note = _pmc_traffic(args.pmc_traffic, dom, args.precision)
+        mfma_busy, mfma_src, mfma_note = _pmc_mfma(args.pmc_mfma, dom, args.precision)
         kernels = {k: {"launches": v[1], "avg_ms": round(v[0] / v[1], 4), "share": round(v[0] / sum(a[0] for a in agg.values()), 3),
                        "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 2), "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1)}
                    for k, v in agg.items()}
@@ -386,11 +419,11 @@ def main():
                          "frac": round(achieved / peak, 4), "peak_basis": basis,
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "traffic_note": traffic_note,
                          "mfma_busy": None if mfma_busy is None else round(mfma_busy, 4),
                          "mfma_busy_basis": "PMC SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), "
                                             "single-stream dispatches (scripts/pmc_mfma.py)",
-                         "mfma_busy_source": mfma_src,
+                         "mfma_busy_source": mfma_src, "mfma_busy_note": mfma_note,
                          "algorithmic_bytes_per_launch": round(tot_by / cnt),
                          "algorithmic_flops_per_launch": round(tot_fl / cnt),
                          "avg_launch_ms": round(avg_s * 1e3, 4), "launches": cnt,

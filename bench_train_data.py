@@ -63,7 +63,7 @@ def main():
     out = {"metric": "AmassDataset training items/s (window 64, noise)", "value": round(a.batch / dt, 1),
            "unit": "items/s", "ms_per_batch": round(dt * 1e3, 4), "batch": a.batch, "n_gpus": 1,
            "regen_frames_per_s": round(n / regen, 1), "regen_ms_per_epoch": round(regen * 1e3, 3),
-           "dtype": "fp32 (FK: f16x3 split MFMA)", "data": f"synthetic: {a.seqs} sequences x {a.frames} frames",
+           "dtype": "fp32 (FK: bf16x3 split MFMA, fp32 range)", "data": f"synthetic: {a.seqs} sequences x {a.frames} frames",
            "config": {"workload": "data_amass.AmassDataset: per-epoch root rotation + SMPL-X FK joints; "
                                   "items = COCO-17 window + noise + target pose"}}
     if not a.no_cpu_baseline:

@@ -78,17 +78,15 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
  * head) serves this call only; tik_ik_forward and tik_stream_create refuse it. */
 int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream);
 
-/* GEMM arithmetic (all accumulate in fp32):
+/* GEMM arithmetic (both accumulate in fp32):
  * 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32);
- * 1 = 3-term f16 split (v_mfma_f32_16x16x32_f16 on x = hi + lo; f16's
- *     exponent range: |x| > 65504 overflows, small values lose bits);
  * 2 = 6-product bf16 split (v_mfma_f32_16x16x32_bf16 on x = p0 + p1 + p2,
  *     products p_i q_j with i + j <= 2: fp32's exponent range, ~2^-24
  *     relative per product) — the DEFAULT.
- * The environment variable TIK_PRECISION=fp32|f16x3|bf16x3 picks the
- * arithmetic at handle creation. */
+ * (1, a 3-term f16 split with f16's narrower range, is retired: the setters
+ * return TIK_E_INVALID for it.) The environment variable
+ * TIK_PRECISION=fp32|bf16x3 picks the arithmetic at handle creation. */
 #define TIK_PREC_F32 0
-#define TIK_PREC_F16X3 1
 #define TIK_PREC_BF16X3 2
 int tik_model_set_precision(tik_model_t m, int prec);
 int tik_model_get_precision(tik_model_t m);

@@ -1,11 +1,9 @@
-# online IK step: grid sweep, eager vs graph, kernel time under rocprofv3
+# online IK step: graph vs eager, kernel time under rocprofv3
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/online; mkdir -p $O
-for g in 16 32 64 128 256; do
-  TIK_ONLINE_GRID=$g timeout -k 10 120 python bench_stream.py --frames 2000 > $O/g$g.json 2> $O/g$g.err || exit $?
-  python -c "import json;d=json.load(open('$O/g$g.json'));print('grid $g', d['value'], d['p99_us'])"
-done
+timeout -k 10 120 python bench_stream.py --frames 2000 > $O/graph.json 2> $O/graph.err || exit $?
+python -c "import json;d=json.load(open('$O/graph.json'));print('graph', d['value'], d['p99_us'])"
 timeout -k 10 120 python bench_stream.py --frames 2000 --no-graph > $O/eager.json 2> $O/eager.err || exit $?
 python -c "import json;d=json.load(open('$O/eager.json'));print('eager', d['value'], d['p99_us'])"
 export TMPDIR=/tmp

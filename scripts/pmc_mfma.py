@@ -16,6 +16,9 @@ import re
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from temporal_inverse_kinematics_amd._build import source_digest  # noqa: E402
+
 
 def main():
     d, out = sys.argv[1:3]
@@ -34,7 +37,7 @@ def main():
         cyc = g / 8.0
         res[k] = {"dispatches": len(busy), "mfma_busy_cycles_per_dispatch": b, "gui_active_per_dispatch": g,
                   "kernel_cycles": cyc, "mfma_busy_frac": b / (cyc * nsimd) if cyc > 0 else None}
-    json.dump({"method": "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE on "
+    json.dump({"source_digest": source_digest(), "method": "rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE on "
                          "'bench.py --steps 3 --warmup 1'; busy / (GRBM_GUI_ACTIVE / 8 x %d SIMDs)" % nsimd,
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():

@@ -14,6 +14,9 @@ import re
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from temporal_inverse_kinematics_amd._build import source_digest  # noqa: E402
+
 
 def per_kernel(d, counter):
     vals = defaultdict(list)
@@ -35,7 +38,7 @@ def main():
         wb = 1024.0 * sum(write.get(k, [0])) / max(1, len(write.get(k, [])))
         res[k] = {"dispatches": len(fetch.get(k, [])), "fetch_bytes_per_dispatch": fb,
                   "write_bytes_per_dispatch": wb, "hbm_bytes_per_dispatch": fb + wb}
-    json.dump({"method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on "
+    json.dump({"source_digest": source_digest(), "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on "
                          "'bench.py --steps 3 --warmup 1'; FETCH_SIZE KB x 1024 x 2 (gfx950 half-count), "
                          "WRITE_SIZE KB x 1024; averaged over the kernel's dispatches",
                "kernels": res}, open(out, "w"), indent=1)

@@ -25,6 +25,22 @@ def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
+def source_digest() -> str:
+    """sha256 over the library's sources (csrc/*.hip, *.cpp, *.h and
+    include/tik.h, by file name and content): names the tree a measurement
+    was taken on. The PMC summaries under profiles/ carry it, and bench.py
+    takes counter fields only from a summary of the tree it benchmarks."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(_sources() + glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(REPO, "include", "tik.h")]
+    for f in files:
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
 def _needs_rebuild(objs_srcs, lib):
     if not os.path.exists(lib):
         return True

@@ -106,12 +106,12 @@ def load(path: str = LIB_PATH):
     return lib
 
 
-PRECISIONS = {"fp32": 0, "f32": 0, "f16x3": 1, "bf16x3": 2}
+PRECISIONS = {"fp32": 0, "f32": 0, "bf16x3": 2}
 
 
 def precision_code(name: str) -> int:
     """'fp32' = exact f32 MFMA; 'bf16x3' = 6-product bf16 split MFMA, fp32 range
-    (the default); 'f16x3' = 3-product f16 split, f16 range (see include/tik.h)."""
+    (the default; see include/tik.h)."""
     if name not in PRECISIONS:
         raise ValueError(f"unknown precision {name!r}; expected one of {sorted(PRECISIONS)}")
     return PRECISIONS[name]

@@ -23,14 +23,13 @@
 
 #include "../../include/tik.h"
 #include "cgemm.h"
-#include "cgemm3.h"
 #include "misc.h"
 #include "online.h"
 #include "common.h"
 #include "xblock.h"
 #include "xgemm.h"
 #include "xgraph.h"
-#include "xtconv.h"
+#include "xtws.h"
 
 namespace tik_host {
 thread_local std::string g_err;
@@ -56,10 +55,10 @@ namespace {
 
 int round4(int c) { return (c + 3) & ~3; }
 
-tik::Seg mkseg(const float* src, const float* w, const SplitW& sw, const SplitW3& s3, int cin, int ld, int kt,
-               int stride, int pad, int tin, int ldw) {
+tik::Seg mkseg(const float* src, const float* w, const SplitW3& s3, int cin, int ld, int kt, int stride, int pad,
+               int tin, int ldw) {
     tik::Seg s{src, w, cin, ld, kt, stride, pad, tin, ldw};
-    s.whi = sw.hi.p; s.wlo = sw.lo.p; s.cin8 = sw.cin8; s.ldw8 = sw.ldw8;
+    s.cin8 = s3.cin8; s.ldw8 = s3.ldw8;
     for (int i = 0; i < 3; ++i) s.wb[i] = s3.p[i].p;
     return s;
 }
@@ -83,23 +82,7 @@ int bn_fold(const TensorMap& m, const std::string& pre, int C, std::vector<float
     return TIK_OK;
 }
 
-typedef unsigned short half_t;   // f16 bit pattern (split-block activations)
-
-tik::Seg3 mkseg3(const half_t* src, int ld, const SBW& w, int kt, int stride, int pad, int tin) {
-    tik::Seg3 s{};
-    s.src = src; s.nblk = w.nblk; s.ld = ld; s.kt = kt; s.stride = stride; s.pad = pad; s.tin = tin;
-    s.w = w.w.p; s.ldw = w.ldw;
-    return s;
-}
-
 enum ResKind { RES_ZERO = 0, RES_IDEN = 1, RES_CONV = 2 };
-
-// debug hook (TIK_DRAIN bitmask): full vmcnt(0) drain before every K-step
-// barrier of the DMA kernels — 1 graph (G), 2 temporal (T), 4 head
-int drain_mask() {
-    static const int m = getenv("TIK_DRAIN") ? atoi(getenv("TIK_DRAIN")) : 0;
-    return m;
-}
 
 // debug (TIK_X_TRACE=1): launch an xgemm with per-workgroup phase stamps and
 // print the averages (s_memtime cycles) to stderr; synchronizes the stream
@@ -131,18 +114,6 @@ hipError_t launch_xgemm_traced(tik::XArgs a, int bn, int epi, hipStream_t st, co
     return e;
 }
 
-// nontemporal stores of the backbone's layer outputs (XArgs::nts): TIK_XNTS = bit mask of
-// the layers that use them (default all; 0 = none)
-static int xnts(int layer) {
-    static const int m = [] { const char* e = getenv("TIK_XNTS"); return e ? atoi(e) : 255; }();
-    return (m >> layer) & 1;
-}
-// tuning experiments on the xgemm kernels (XArgs::tune), TIK_XTUNE=<bits>; 0 in production
-int xtune() {
-    static const int t = getenv("TIK_XTUNE") ? atoi(getenv("TIK_XTUNE")) : 0;
-    return t;
-}
-
 thread_local Profiler* g_prof = nullptr;   // set for the duration of a profiled call
 
 // debug (TIK_CHECKSUM=1): after every annotated launch, synchronise and
@@ -166,8 +137,6 @@ struct ProfScope {
     }
     ~ProfScope() {
         if (g_prof) g_prof->end(i, st);
-        static const bool sync_each = getenv("TIK_SYNC_EACH") != nullptr;   // debug: serialise launches
-        if (sync_each) (void)hipStreamSynchronize(st);
         if (checksum_mode() && op) {
             if (!g_cks_dev) (void)hipMalloc(&g_cks_dev, 8);
             unsigned long long h = 0;
@@ -218,21 +187,15 @@ struct Layer {
     DevBuf wt;      // [cout][3*cout]        tcn conv scaled by tcn.3 BN, k = tap*cout + ci
     DevBuf wr;      // [cout][cinp]          residual conv scaled by residual.1 BN
     DevBuf biasT;   // [cout]                tcn bias (+ residual bias) folded
-    SplitW swg, swt, swr;   // f16 hi/lo planes of wg, wt, wr (PREC_F16X3, register-staged path)
-    SplitW3 s3g, s3t, s3r;  // bf16 planes p0+p1+p2 of wg, wt, wr (PREC_BF16X3)
-    SBW sbg, sbt, sbr;      // split-block copies (PREC_F16X3, DMA path)
+    SplitW3 s3g, s3t, s3r;  // bf16 planes p0+p1+p2 of wg, wt, wr (cgemm.hip: tik_stgcn_block_fwd, small batches)
     DevBuf wr0;             // [cout][cin] residual conv for a raw-input first layer (cin <= 4)
     DevHBuf xg, xt;         // bf16x3 tiles of the gcn (cin % 32 == 0) and of tcn (+ residual conv) (xgemm.hip)
-    DevHBuf xtw;            // resident-weight temporal conv (xtconv.hip, 128 -> 128, stride 1, identity residual)
+    DevHBuf xtw;            // weight-stationary temporal conv (xtws.hip, 128 -> 128, stride 1, identity residual)
     DevHBuf xgw;            // weight-stationary gcn kernel (xgraph.hip, 128 / 256 output channels): gcn planes in the MFMA register layout
     DevHBuf xbg, xbt;       // whole-block kernel (xblock.hip, 64 channels, stride 1): gcn / tcn planes in the MFMA register layout
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
-    int xnw = 4;            // xgemm waves per workgroup (TIK_XNW=8: one 256-row workgroup per CU)
-    int xepi = 2;           // xgemm EPI_BIAS epilogue: 1 through LDS, whole-line stores; 2 (default) + identity residual loaded there; 0 from registers (TIK_XEPI)
-    int xpt = 0;            // temporal conv on the persistent cross-tile kernel (launch_xgemm_pt; default for 64-column layers; TIK_XPT bit mask of layers)
-    int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers)
+    int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers; 0 = the XG tiles)
     int xtwson = 1;         // temporal conv on xtws.hip where packed (TIK_XTWS bit mask of layers; 0 = XT128)
-    int xtcon = 0;          // temporal conv on xtconv.hip where packed (TIK_XTC bit mask of layers; off: measured 1-2 % slower than XT128)
     int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
@@ -290,8 +253,7 @@ struct Layer {
                 hbt[co] += (float)((double)scr[co] * (br ? br->v[co] : 0.0) + shr[co]);
             }
             wr_host = hwr;
-            if ((rc = wr.upload(hwr)) || (rc = swr.build(hwr, cout, 1, cinp, cinp)) || (rc = sbr.build(hwr, cout, 1, cinp, cinp)) ||
-                (rc = s3r.build(hwr, cout, 1, cinp, cinp)))
+            if ((rc = wr.upload(hwr)) || (rc = s3r.build(hwr, cout, 1, cinp, cinp)))
                 return rc;
             if (cin <= 4) {
                 std::vector<float> h0((size_t)cout * cin);
@@ -313,7 +275,7 @@ struct Layer {
                 if ((rc = xt.upload(tik::xgemm_pack(t, ns, cout, bn)))) return rc;
                 xt_bn = bn; xt_ks = TK * cout / 32 + (ns == 2 ? cin / 32 : 0);
             }
-            if (cout == 128 && cin == 128 && stride == 1 && res == RES_IDEN && V == 17)   // xtconv.hip
+            if (cout == 128 && cin == 128 && stride == 1 && res == RES_IDEN && V == 17)   // xtws.hip
                 if ((rc = xtw.upload(tik::xblock_pack_weights(hwt.data(), cout, TK * cout, TK, cout)))) return rc;
             if ((cout == 128 || cout == 256) && (cin == 64 || cin == 128 || cin == 256) && V == 17)   // xgraph.hip
                 if ((rc = xgw.upload(tik::xblock_pack_weights(hwg.data(), cout, cinp, 1, cin)))) return rc;
@@ -325,9 +287,7 @@ struct Layer {
         std::vector<float> ha(A_eff.begin(), A_eff.end());
         mix_sparse = tik::fits_coco_hop2(ha.data(), V);
         if ((rc = wg.upload(hwg)) || (rc = bias2.upload(hb2)) || (rc = amix.upload(ha)) || (rc = wt.upload(hwt)) ||
-            (rc = biasT.upload(hbt)) || (rc = swg.build(hwg, cout, 1, cinp, cinp)) ||
-            (rc = swt.build(hwt, cout, TK, cout, TK * cout)) || (rc = sbg.build(hwg, cout, 1, cinp, cinp)) ||
-            (rc = sbt.build(hwt, cout, TK, cout, TK * cout)) || (rc = s3g.build(hwg, cout, 1, cinp, cinp)) ||
+            (rc = biasT.upload(hbt)) || (rc = s3g.build(hwg, cout, 1, cinp, cinp)) ||
             (rc = s3t.build(hwt, cout, TK, cout, TK * cout)))
             return rc;
         return TIK_OK;
@@ -342,7 +302,7 @@ struct Layer {
         const int to = tout(tin, stride);
         tik::CgemmArgs g{};
         g.M = N * tin * V; g.Nc = cout; g.V = V; g.tout = tin;
-        g.seg[0] = mkseg(x, wg.p, swg, s3g, cinp, ld, 1, 1, 0, tin, cinp);
+        g.seg[0] = mkseg(x, wg.p, s3g, cinp, ld, 1, 1, 0, tin, cinp);
         g.nseg = 1;
         g.bias = bias2.p; g.out = z; g.ldo = cout; g.amix = amix.p; g.act = tik::ACT_RELU;
         g.mix_sparse = mix_sparse ? 1 : 0;
@@ -356,10 +316,10 @@ struct Layer {
 
         tik::CgemmArgs t{};
         t.M = N * to * V; t.Nc = cout; t.V = V; t.tout = to;
-        t.seg[0] = mkseg(z, wt.p, swt, s3t, cout, cout, TK, stride, 1, tin, TK * cout);
+        t.seg[0] = mkseg(z, wt.p, s3t, cout, cout, TK, stride, 1, tin, TK * cout);
         t.nseg = 1;
         if (res == RES_CONV) {
-            t.seg[1] = mkseg(x, wr.p, swr, s3r, cinp, ld, 1, stride, 0, tin, cinp);
+            t.seg[1] = mkseg(x, wr.p, s3r, cinp, ld, 1, stride, 0, tin, cinp);
             t.nseg = 2;
         } else if (res == RES_IDEN) {
             t.resid = x; t.ldr = ld;
@@ -370,7 +330,7 @@ struct Layer {
         if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
         if (res == RES_IDEN) by += 4.0 * px_out * cout;
         {
-            // 64-channel layers: 256x64 tiles for fp32; 128x64 for f16x3 (two register
+            // 64-channel layers: 256x64 tiles for fp32; 128x64 for bf16x3 (two register
             // staging sets of a 256-row tile would cost a wave per SIMD)
             const int cfg = big ? tik::CFG_T128x128 : (prec == tik::PREC_F32 ? tik::CFG_T256x64 : tik::CFG_T128x64);
             const std::string lab = std::string(big ? "T128x128.L" : (cfg == tik::CFG_T256x64 ? "T256x64.L" : "T128x64.L")) +
@@ -406,7 +366,7 @@ struct Layer {
             tik::XGraphArgs g{};
             g.nframes = N * tin; g.x = x; g.ldx = ld; g.cin = cin; g.cout = cout; g.wp = xgw.p;
             g.bias2 = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout;
-            g.nts = xnts(index); g.trash = xtrash; g.tune = xtune();
+            g.nts = 1; g.trash = xtrash;
             const std::string lab = "XGW.L" + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
@@ -418,33 +378,22 @@ struct Layer {
             g.seg[0] = tik::XSeg{x, ld, cin, 1, 1, 0, tin, rin};
             g.nseg = 1; g.wp = xg.p; g.ksteps = xg_ks;
             g.bias = bias2.p; g.amix = amix.p; g.mix_sparse = mix_sparse ? 1 : 0; g.out = z; g.ldo = cout; g.act = tik::ACT_RELU;
-            g.tune = xtune(); g.nw = xnw; g.nts = xnts(index);
+            g.nw = 4; g.nts = 1;
             const std::string lab = std::string(xg_bn == 128 ? "XG128.L" : "XG64.L") + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
                         4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
-        if (xtwson && !xtcon && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0) {
+        if (xtwson && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0) {
             tik::XTConvArgs c{};
             c.M = (int)rout; c.T = tin; c.z = z; c.ldz = cout; c.x = x; c.ldx = ld; c.wp = xtw.p; c.bias = biasT.p;
-            c.out = out; c.ldo = cout; c.nts = xnts(index); c.trash = xtrash; c.tune = xtune();
+            c.out = out; c.ldo = cout; c.nts = 1; c.trash = xtrash;
             const std::string lab = "XTW.L" + std::to_string(index);
             ProfScope p(lab.c_str(), 2.0 * px_out * TK * cout * cout,
                         4.0 * (px_in * cout + 2.0 * px_out * cout + (double)TK * cout * cout), st);
             p.out(out, (size_t)rout * cout * 4);
             HIP_TRY(tik::launch_xtws(c, ncu, st));
-            return TIK_OK;
-        }
-        if (xtcon && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0) {
-            tik::XTConvArgs c{};
-            c.M = (int)rout; c.T = tin; c.z = z; c.ldz = cout; c.x = x; c.ldx = ld; c.wp = xtw.p; c.bias = biasT.p;
-            c.out = out; c.ldo = cout; c.nts = xnts(index); c.trash = xtrash; c.tune = xtune();
-            const std::string lab = "XTC.L" + std::to_string(index);
-            ProfScope p(lab.c_str(), 2.0 * px_out * TK * cout * cout,
-                        4.0 * (px_in * cout + 2.0 * px_out * cout + (double)TK * cout * cout), st);
-            p.out(out, (size_t)rout * cout * 4);
-            HIP_TRY(tik::launch_xtconv(c, ncu, st));
             return TIK_OK;
         }
         tik::XArgs t{};
@@ -466,9 +415,11 @@ struct Layer {
         t.wp = xt.p; t.ksteps = tik::xgemm_ksteps(t);
         if (tik::xgemm_kmain(t) != xt_ks) return fail(TIK_E_INVALID, "layer %d: xgemm K steps %d != packed %d", index, tik::xgemm_kmain(t), xt_ks);
         t.bias = biasT.p; t.out = out; t.ldo = cout; t.act = tik::ACT_RELU;
-        t.tune = xtune(); t.nw = xnw; t.epi_lds = xepi != 0; t.idn_epi = xepi == 2; t.nts = xnts(index);
+        t.nw = 4; t.epi_lds = 1; t.idn_epi = 1; t.nts = 1;
         t.trash = xtrash;
-        const bool pt = xpt && xtrash && xnw != 8 && cout % xt_bn == 0 && !(res == RES_IDEN && !t.idn_epi);
+        // the 64-column temporal convs (6 K steps per tile) on the persistent kernel: it hides
+        // the first-DMA prologue that is a large share of such short tiles
+        const bool pt = xt_bn == 64 && xtrash && cout % xt_bn == 0;
         const std::string lab = std::string(xt_bn == 128 ? (pt ? "XP128.L" : "XT128.L") : (pt ? "XP64.L" : "XT64.L")) +
                                 std::to_string(index);
         ProfScope p(lab.c_str(), fl, by, st);
@@ -478,283 +429,6 @@ struct Layer {
             HIP_TRY(tik::launch_xgemm_pt(t, xt_bn, ncu, st));
         } else {
             HIP_TRY(launch_xgemm_traced(t, xt_bn, tik::EPI_BIAS, st, lab.c_str()));
-        }
-        return TIK_OK;
-    }
-
-    // f16x3 on split-block activations (cgemm3.hip, DMA-staged). x: SB rows
-    // [N*tin*V][ld] halves; z / out: SB rows of 64*ceil(cout/32) halves.
-    // Raw-input first layer (cin <= 4, residual conv, stride 1): the data_bn'd
-    // keypoints feed the gcn (layer0.hip) and the residual conv (tcn epilogue)
-    // directly, no split-block input.
-    bool raw_ok() const {
-        return index == 0 && cin <= 4 && res == RES_CONV && stride == 1 && wr0.p && cout >= 16 && cout % 4 == 0 &&
-               256 % (cout / 4) == 0;
-    }
-
-    // this block's temporal conv can carry block n's gcn in its epilogue
-    // (TG_128x128_G7: 128 output channels in one tile; n: 128 -> 128, not a raw/whole-block layer)
-    bool can_fuse_next(const Layer& n) const {
-        return V == 17 && n.V == 17 && cout == 128 && n.cin == 128 && n.cout == 128 && n.index != 0 && sbt.nblk == 4 &&
-               n.sbg.nblk == 4;
-    }
-
-    int forward3(const half_t* x, int ld, int N, int tin, half_t* z, half_t* out, const half_t* zeros, hipStream_t st,
-                 bool use_halo = false, const float* xraw = nullptr, const float* bn_sc = nullptr,
-                 const float* bn_sh = nullptr, float* xb4 = nullptr, bool fuse = true, const Layer* nxt = nullptr,
-                 half_t* znext = nullptr, bool zready = false, half_t* trash = nullptr,
-                 half_t* gtrash = nullptr) const {
-        const int ldz = 64 * sbt.nblk;
-        const int to = tout(tin, stride);
-        const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
-        tik::Cgemm3Args g{};
-        g.M = (int)rin; g.Nc = cout; g.V = V; g.tout = tin;
-        g.seg[0] = mkseg3(x, ld, sbg, 1, 1, 0, tin);
-        g.nseg = 1;
-        g.bias = bias2.p; g.out_h = z; g.ldo = ldz; g.amix = amix.p; g.act = tik::ACT_RELU;
-        g.mix_sparse = mix_sparse ? 1 : 0; g.zeros = zeros;
-        if (drain_mask() & 1) g.tune |= 2;
-        const double px_in = (double)rin, px_out = (double)rout;
-        if (!xraw && stride == 1 && res == RES_IDEN && V == 17 && tik::stblock_ok(cin, cout) && fuse) {
-            // whole block in one kernel: z stays in LDS (stblock.hip)
-            tik::StbArgs b{};
-            b.x = x; b.ldx = ld; b.nwin = N; b.T = tin;
-            b.wg = sbg.w.p; b.ldwg = sbg.ldw; b.bias2 = bias2.p; b.amix = amix.p; b.mix_sparse = mix_sparse ? 1 : 0;
-            b.wt = sbt.w.p; b.ldwt = sbt.ldw; b.bias = biasT.p; b.resid = 1; b.out = out; b.ldo = ldz;
-            const std::string lab = std::string("B3_") + std::to_string(cout) + ".L" + std::to_string(index);
-            ProfScope p(lab.c_str(),
-                        2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * TK * cout * cout,
-                        4.0 * (px_in * cin + px_out * cout + (double)cout * cin + (double)TK * cout * cout), st);
-            static const bool trace = getenv("TIK_STB_TRACE") != nullptr;
-            if (!trace) {
-                p.out(out, (size_t)rout * ldz * 2);
-                HIP_TRY(tik::launch_stblock(b, cin, cout, st));
-                return TIK_OK;
-            }
-            // debug hook: per-phase workgroup timing (G, y store, mix, T, epilogue), printed to stderr
-            const int F = 14;
-            const int ntl = (N * tin + F - 1) / F;
-            const int nwg = 1024;   // >= the persistent grid; unused entries stay zero
-            unsigned long long* d = nullptr;
-            HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
-            HIP_TRY(hipMemset(d, 0, (size_t)nwg * 6 * 8));
-            b.trace = d;
-            HIP_TRY(tik::launch_stblock(b, cin, cout, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            std::vector<unsigned long long> h((size_t)nwg * 6);
-            HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-            HIP_TRY(hipFree(d));
-            double ph[5] = {0, 0, 0, 0, 0};
-            for (int w = 0; w < nwg; ++w)
-                for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
-            fprintf(stderr, "stblock L%d (%d tiles): per-tile us G %.2f wt-issue %.2f mix %.2f T %.2f epi %.2f\n",
-                    index, ntl, ph[0] / ntl / 100, ph[1] / ntl / 100, ph[2] / ntl / 100, ph[3] / ntl / 100,
-                    ph[4] / ntl / 100);
-            return TIK_OK;
-        }
-        if (xraw && fuse && stride == 1 && res == RES_CONV && V == 17 && cout == 64 && wr0.p) {
-            // the whole first block from the raw keypoints in one kernel (stblock.hip, RAW)
-            tik::StbArgs b{};
-            b.nwin = N; b.T = tin;
-            b.bias2 = bias2.p; b.amix = amix.p; b.mix_sparse = mix_sparse ? 1 : 0;
-            b.wt = sbt.w.p; b.ldwt = sbt.ldw; b.bias = biasT.p; b.out = out; b.ldo = ldz;
-            b.xraw = xraw; b.c0 = cin; b.bn_sc = bn_sc; b.bn_sh = bn_sh; b.wg0 = wg.p; b.ldwg0 = cinp; b.rw = wr0.p;
-            ProfScope p("B0_64.L0",
-                        2.0 * px_in * cin * cout + 2.0 * V * px_in * cout + 2.0 * px_out * (TK * cout + cin) * cout,
-                        4.0 * (px_in * cin + px_out * cout + (double)TK * cout * cout), st);
-            p.out(out, (size_t)rout * ldz * 2);
-            static const bool trace0 = getenv("TIK_STB_TRACE") != nullptr;   // debug: per-phase workgroup timing
-            const int ntl = (N * tin + 13) / 14;
-            const int nwg = 1024;   // >= the persistent grid
-            unsigned long long* d = nullptr;
-            if (trace0) {
-                HIP_TRY(hipMalloc(&d, (size_t)nwg * 6 * 8));
-                HIP_TRY(hipMemset(d, 0, (size_t)nwg * 6 * 8));
-                b.trace = d;
-            }
-            HIP_TRY(tik::launch_stblock0(b, cout, st));
-            if (trace0) {
-                HIP_TRY(hipStreamSynchronize(st));
-                std::vector<unsigned long long> h((size_t)nwg * 6);
-                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                HIP_TRY(hipFree(d));
-                double ph[5] = {0, 0, 0, 0, 0};
-                for (int w = 0; w < nwg; ++w)
-                    for (int k = 0; k < 5; ++k) ph[k] += (double)(h[6 * w + k + 1] - h[6 * w + k]);
-                fprintf(stderr, "stblock0 L0 (%d tiles): per-tile us G(raw) %.2f - %.2f wt-issue %.2f T %.2f epi %.2f\n", ntl,
-                        ph[0] / ntl / 100, ph[1] / ntl / 100, ph[2] / ntl / 100, ph[3] / ntl / 100, ph[4] / ntl / 100);
-            }
-            return TIK_OK;
-        }
-        if (zready) {
-            // z was written by the previous block's fused temporal-conv epilogue
-        } else if (xraw) {
-            ProfScope p("G0_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
-                        4.0 * (px_in * cin + px_in * cout), st);
-            p.out(z, (size_t)rin * ldz * 2);
-            HIP_TRY(tik::launch_gcn0(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
-                                     cout, z, ldz, xb4, st));
-        } else {
-            g.trash = gtrash;
-            if (gtrash && tik::gpw_ok(g)) {
-                // weight-stationary persistent gcn: the next tile's x streams in behind this one (gpw.hip)
-                const std::string lab = std::string("GP_") + std::to_string(cout) + ".L" + std::to_string(index);
-                ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
-                            4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
-                p.out(z, (size_t)rin * ldz * 2);
-                static const bool gtr = getenv("TIK_G_TRACE") != nullptr;   // debug: per-tile phase timing
-                unsigned long long* d = nullptr;
-                if (gtr) {
-                    HIP_TRY(hipMalloc(&d, (size_t)1024 * 8 * 8));
-                    HIP_TRY(hipMemset(d, 0, (size_t)1024 * 8 * 8));
-                    g.trace = d;
-                }
-                HIP_TRY(tik::launch_gpw(g, st));
-                if (gtr) {
-                    HIP_TRY(hipStreamSynchronize(st));
-                    std::vector<unsigned long long> h((size_t)1024 * 8);
-                    HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                    HIP_TRY(hipFree(d));
-                    double ph[6] = {0, 0, 0, 0, 0, 0}, tiles = 0;
-                    for (int w = 0; w < 1024; ++w) {
-                        tiles += (double)h[8 * w];
-                        for (int k = 0; k < 6; ++k) ph[k] += (double)h[8 * w + 1 + k];
-                    }
-                    tiles = std::max(1.0, tiles);
-                    fprintf(stderr, "GP L%d (%.0f tiles): per-tile us wait %.2f (issue %.2f, vmcnt %.2f) mfma %.2f y-stage %.2f mix+stores %.2f\n",
-                            index, tiles, ph[0] / tiles / 100, ph[4] / tiles / 100, ph[5] / tiles / 100, ph[1] / tiles / 100,
-                            ph[2] / tiles / 100, ph[3] / tiles / 100);
-                }
-                goto temporal;
-            }
-            // 128-column tiles (8 waves) read each input row once per 128 outputs
-            const bool wide = cout % 128 == 0;
-            const std::string lab = std::string(wide ? "G3_272x128.L" : "G3_272x64.L") + std::to_string(index);
-            ProfScope p(lab.c_str(), 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout,
-                        4.0 * (px_in * cin + px_in * cout + (double)cout * cin + (double)V * (V + cout)), st);
-            p.out(z, (size_t)rin * ldz * 2);
-            static const bool gtrace = getenv("TIK_G_TRACE") != nullptr;   // debug: per-workgroup loop / epilogue time
-            const int nwg = (int)((rin + 271) / 272) * ((cout + (wide ? 127 : 63)) / (wide ? 128 : 64));
-            unsigned long long* d = nullptr;
-            if (gtrace) {
-                HIP_TRY(hipMalloc(&d, (size_t)nwg * 5 * 8));
-                g.trace = d;
-            }
-            HIP_TRY(tik::launch_cgemm3(g, wide ? tik::C3_G272x128_W8 : tik::C3_G272x64, st));
-            if (gtrace) {
-                HIP_TRY(hipStreamSynchronize(st));
-                std::vector<unsigned long long> h((size_t)nwg * 5);
-                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                HIP_TRY(hipFree(d));
-                double loop = 0, epi = 0, vmw = 0;
-                unsigned long long lo = ~0ull, hi = 0;
-                for (int w = 0; w < nwg; ++w) {
-                    loop += (double)(h[5 * w + 1] - h[5 * w]);
-                    epi += (double)(h[5 * w + 2] - h[5 * w + 1]);
-                    vmw += (double)h[5 * w + 3];
-                    lo = std::min(lo, h[5 * w]); hi = std::max(hi, h[5 * w + 2]);
-                }
-                fprintf(stderr, "G L%d (%d wg): per-wg us loop %.2f epilogue %.2f (wave0 DMA wait %.0f cycles) | span %.1f us\n",
-                        index, nwg, loop / nwg / 100, epi / nwg / 100, vmw / nwg, (hi - lo) / 100.0);
-            }
-        }
-    temporal:
-        tik::Cgemm3Args t{};
-        t.M = (int)rout; t.Nc = cout; t.V = V; t.tout = to;
-        t.seg[0] = mkseg3(z, ldz, sbt, TK, stride, 1, tin);
-        t.nseg = 1;
-        if (xraw) {
-            t.rx = xb4; t.rxc = cin; t.rw = wr0.p;
-        } else if (res == RES_CONV) {
-            t.seg[1] = mkseg3(x, ld, sbr, 1, stride, 0, tin);
-            t.nseg = 2;
-        } else if (res == RES_IDEN) {
-            t.resid = x; t.ldr = ld;
-        }
-        t.bias = biasT.p; t.out_h = out; t.ldo = ldz; t.act = tik::ACT_RELU;
-        t.zeros = zeros;
-        if (drain_mask() & 2) t.tune |= 2;
-        const bool big = cout >= 128;
-        double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + px_out * cout + (double)TK * cout * cout);
-        if (res == RES_CONV) { fl += 2.0 * px_out * cin * cout; by += 4.0 * (px_out * cin + (double)cin * cout); }
-        if (res == RES_IDEN) by += 4.0 * px_out * cout;
-        if (nxt) {
-            // + the next block's gcn in the epilogue (TG_128x128_G7): its z is written here
-            t.g_w = nxt->sbg.w.p; t.g_ldw = nxt->sbg.ldw; t.g_nc = nxt->cout; t.g_bias2 = nxt->bias2.p;
-            t.g_amix = nxt->amix.p; t.g_mix_sparse = nxt->mix_sparse ? 1 : 0; t.g_out = znext;
-            t.g_ldo = 64 * nxt->sbt.nblk;
-            fl += 2.0 * px_out * cout * nxt->cout + 2.0 * V * px_out * nxt->cout;
-            by += 4.0 * (px_out * nxt->cout + (double)nxt->cout * cout + (double)V * (V + nxt->cout));
-            t.trash = trash;
-            if (trash && tik::tgw_ok(t)) {
-                // stride 1 + identity residual: the weight-stationary persistent kernel (tgw.hip)
-                const std::string lab = std::string("TW_128.L") + std::to_string(index);
-                static const bool trace = getenv("TIK_TG_TRACE") != nullptr;   // debug: per-phase workgroup timing
-                const int grid = 256;
-                unsigned long long* d = nullptr;
-                if (trace) {
-                    HIP_TRY(hipMalloc(&d, (size_t)1024 * 8 * 8));
-                    HIP_TRY(hipMemset(d, 0, (size_t)1024 * 8 * 8));
-                    t.trace = d;
-                }
-                {
-                    ProfScope p(lab.c_str(), fl, by, st);
-                    p.out(out, (size_t)rout * ldz * 2);
-                    HIP_TRY(tik::launch_tgw(t, st));
-                }
-                if (trace) {
-                    HIP_TRY(hipStreamSynchronize(st));
-                    std::vector<unsigned long long> h((size_t)1024 * 8);
-                    HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                    HIP_TRY(hipFree(d));
-                    double ph[7] = {0, 0, 0, 0, 0, 0, 0}, tiles = 0;
-                    int nwg = 0;
-                    for (int w = 0; w < 1024; ++w) {
-                        if (!h[8 * w + 5]) continue;
-                        ++nwg; tiles += (double)h[8 * w];
-                        for (int k = 0; k < 7; ++k) ph[k] += (double)h[8 * w + 1 + k];
-                    }
-                    (void)grid;
-                    fprintf(stderr, "TW L%d (%d wg, %.1f tiles/wg): per-tile us loop %.2f epi-image %.2f (E1 wait %.2f, barrier %.2f) epi-gcn %.2f epi-mix %.2f | per-wg span %.1f us\n",
-                            index, nwg, tiles / std::max(1, nwg), ph[0] / tiles / 100, ph[1] / tiles / 100, ph[5] / tiles / 100,
-                            ph[6] / tiles / 100, ph[2] / tiles / 100, ph[3] / tiles / 100, ph[4] / std::max(1, nwg) / 100);
-                }
-                return TIK_OK;
-            }
-            const std::string lab = std::string("TG3_128x128.L") + std::to_string(index);
-            static const bool trace = getenv("TIK_TG_TRACE") != nullptr;   // debug: per-phase workgroup timing
-            const int nwg = (int)((rout + 118) / 119);
-            unsigned long long* d = nullptr;
-            if (trace) {
-                HIP_TRY(hipMalloc(&d, (size_t)nwg * 8 * 8));
-                t.trace = d;
-            }
-            {
-                ProfScope p(lab.c_str(), fl, by, st);
-                p.out(out, (size_t)rout * ldz * 2);
-                HIP_TRY(tik::launch_tgemm(t, tik::TG_128x128_G7, st));
-            }
-            if (trace) {
-                HIP_TRY(hipStreamSynchronize(st));
-                std::vector<unsigned long long> h((size_t)nwg * 8);
-                HIP_TRY(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-                HIP_TRY(hipFree(d));
-                double ph[7] = {0, 0, 0, 0, 0, 0, 0};
-                for (int w = 0; w < nwg; ++w)
-                    for (int k = 0; k < 7; ++k) ph[k] += (double)(h[8 * w + k + 1] - h[8 * w + k]);
-                fprintf(stderr, "TG L%d (%d wg): per-wg us loop %.2f stageC %.2f image+Wg %.2f gcn %.2f out+stageZ %.2f mix %.2f tail %.2f\n",
-                        index, nwg, ph[0] / nwg / 100, ph[1] / nwg / 100, ph[2] / nwg / 100, ph[3] / nwg / 100,
-                        ph[4] / nwg / 100, ph[5] / nwg / 100, ph[6] / nwg / 100);
-            }
-        } else if (use_halo && tik::tconv_halo_ok(t)) {   // stride 1: taps share one LDS frame halo (tconv.hip)
-            const std::string lab = std::string(big ? "TH_128x128.L" : "TH_128x64.L") + std::to_string(index);
-            ProfScope p(lab.c_str(), fl, by, st);
-            HIP_TRY(tik::launch_tconv_halo(t, big ? 128 : 64, st));
-        } else {
-            const std::string lab = std::string(big ? "T3_128x128.L" : "T3_128x64.L") + std::to_string(index);
-            ProfScope p(lab.c_str(), fl, by, st);
-            p.out(out, (size_t)rout * ldz * 2);
-            HIP_TRY(tik::launch_tgemm(t, big ? tik::TG_128x128 : tik::TG_128x64, st));
         }
         return TIK_OK;
     }
@@ -768,40 +442,29 @@ struct tik_model {
     std::vector<Layer> layers;
     DevBuf bn_sc, bn_sh;           // data_bn (V*C0)
     DevBuf w0, b0, w3, b3;         // head
-    SplitW sw0, sw3;
     SplitW3 s30, s33;
-    SBW sb0, sb3;
     DevHBuf xh0;                   // bf16x3 tiles of pose_regressor.0 for xgemm.hip (feat % 32 == 0)
-    int xhead_ks = 4;              // xgemm head: K slices, fixed so a window's poses do not depend on the batch size (TIK_XHEAD_KS; 0: the cgemm head)
-    int prec = 1;
-    // ws[0]: the handle's workspace (z, z2: ping-pong for the fused T+G launches);
-    // ws[1] + a private stream: large f16x3 batches run as two halves on two
-    // streams, so one half's launches fill the other's tails and epilogues.
-    // Online-IK streams own their workspaces (stream.cpp).
-    static constexpr int MAXSPLIT = 4;
+    int xhead_ks = 4;              // xgemm head: K slices, fixed so a window's poses do not depend on the batch size
+    int prec = 2;
+    // ws[0]: the handle's workspace; ws[1] + a private stream: large batches run
+    // as two parts on two streams, so one part's HBM-bound launches run beside
+    // the other's MFMA-bound ones. Online-IK streams own their workspaces (stream.cpp).
+    static constexpr int MAXSPLIT = 2;
     Workspace ws[MAXSPLIT];
     hipStream_t aux[MAXSPLIT - 1] = {};
     hipEvent_t ev_fork = nullptr, ev_join[MAXSPLIT - 1] = {};
     bool split = true;                 // TIK_SPLIT=0: one stream
-    int nsplit = 2;                    // parts of a split batch (TIK_SPLIT_N, 2..4)
+    int nsplit = 2;                    // parts of a split batch
     std::atomic<int> refs{1};          // the handle + every live online-IK stream
     ~tik_model() {
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (auto e : ev_join) if (e) (void)hipEventDestroy(e);
         for (auto a : aux) if (a) (void)hipStreamDestroy(a);
     }
-    DevHBuf zeros;                 // zero source for padded rows (cgemm3 DMA)
-    long long dma_min_frames = 1;      // f16x3: N*T at or above -> split-activation DMA path (TIK_GEMM_PATH)
-    int small_head_rows = 256;         // DMA path: output rows at or below -> split-K head (TIK_SMALL_HEAD)
-    int dma_chunk_max = 0;             // test hook (TIK_DMA_CHUNK): cap on windows per DMA sub-batch
-    bool stblock = true;               // whole-block kernel for stride-1 identity blocks (TIK_STBLOCK=0: G + T)
-    bool fuse_tg = true;               // next block's gcn in the temporal-conv epilogue (TIK_FUSE_TG=0: off)
-    bool tgw = true;                   // stride-1 fused blocks on the weight-stationary kernel (TIK_TGW=0: TG3)
-    bool gpw = true;                   // unfused gcn launches on the persistent kernel (TIK_GPW=0: G3_272x128)
-    bool xgemm = true;                 // bf16x3 backbone on xgemm.hip (TIK_XGEMM=0: register-staged cgemm.hip)
+    int x_chunk_max = 0;               // test hook (TIK_X_CHUNK): cap on windows per sub-batch
     bool xblk = true;                  // blocks 0 and 1 as whole-block kernels (xblock.hip; TIK_XBLK=0: layered G + T)
     int ncu = 256;                     // compute units (persistent grids)
-    DevHBuf trash;                     // scratch line for the tgw kernel's stores of invalid rows
+    DevHBuf trash;                     // scratch line for the persistent kernels' stores of invalid rows
     Profiler prof;
     bool profiling = false;
 };
@@ -814,48 +477,25 @@ struct ProfGuard {
 struct tik_block {
     Layer layer;
     DevBuf xp, z;   // padded-input and z workspace
-    int prec = 1;
+    int prec = 2;
 };
 
-// handle settings read from the environment (A/B and test hooks) and the
-// device facts the launches need; the same for full and backbone-only handles
+// handle settings read from the environment (each selects a test-pinned
+// alternative of the default path) and the device facts the launches need;
+// the same for full and backbone-only handles
 static void apply_env(tik_model* md) {
-    if (const char* e = getenv("TIK_DMA_CHUNK")) md->dma_chunk_max = atoi(e);
-    if (const char* e = getenv("TIK_STBLOCK")) md->stblock = e[0] != '0';
-    if (const char* e = getenv("TIK_FUSE_TG")) md->fuse_tg = e[0] != '0';
-    if (const char* e = getenv("TIK_TGW")) md->tgw = e[0] != '0';
-    if (const char* e = getenv("TIK_GPW")) md->gpw = e[0] != '0';
-    if (const char* e = getenv("TIK_XGEMM")) md->xgemm = e[0] != '0';
+    if (const char* e = getenv("TIK_X_CHUNK")) md->x_chunk_max = atoi(e);
     if (const char* e = getenv("TIK_XBLK")) md->xblk = e[0] != '0';
-    if (const char* e = getenv("TIK_XNW"))
-        for (auto& L : md->layers) L.xnw = atoi(e) == 8 ? 8 : 4;
-    if (const char* e = getenv("TIK_XEPI"))
-        for (auto& L : md->layers) L.xepi = atoi(e);
-    {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
-            for (auto& L : md->layers) L.ncu = ncu;
-            md->ncu = ncu;
-        }
-        const char* e = getenv("TIK_XPT");
-        for (auto& L : md->layers) {
-            // default: the 64-column temporal convs (6 K steps per tile: the
-            // prologue the persistent kernel hides is a large share); TIK_XPT: bit l = layer l
-            L.xpt = e ? (atoi(e) >> L.index) & 1 : (L.xt_bn == 64 ? 1 : 0);
-            if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
-            if (const char* w = getenv("TIK_XTC")) L.xtcon = (atoi(w) >> L.index) & 1;
-            if (const char* w = getenv("TIK_XTWS")) L.xtwson = (atoi(w) >> L.index) & 1;
-            L.xtrash = reinterpret_cast<float*>(md->trash.p);
-        }
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+        md->ncu = ncu;
+    for (auto& L : md->layers) {
+        L.ncu = md->ncu;
+        if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
+        if (const char* w = getenv("TIK_XTWS")) L.xtwson = (atoi(w) >> L.index) & 1;
+        L.xtrash = reinterpret_cast<float*>(md->trash.p);
     }
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
-    if (const char* e = getenv("TIK_SPLIT_N")) md->nsplit = std::min(tik_model::MAXSPLIT, std::max(2, atoi(e)));
-    if (const char* e = getenv("TIK_SMALL_HEAD")) md->small_head_rows = atoi(e);
-    if (const char* e = getenv("TIK_GEMM_PATH")) {   // test hook: force one of the two f16x3 GEMM paths
-        if (!strcmp(e, "dma")) md->dma_min_frames = 1;
-        else if (!strcmp(e, "reg")) md->dma_min_frames = -1;
-    }
-    if (const char* e = getenv("TIK_XHEAD_KS")) md->xhead_ks = std::min(8, atoi(e));
 }
 
 extern "C" {
@@ -901,7 +541,7 @@ int tik_debug_check_guards(void) {
     g_err = rep;
     return bad;
 }
-const char* tik_version(void) { return "tik 0.3.0 (gfx950; bf16x3 split MFMA (default, fp32 range), exact fp32 MFMA, f16x3 split MFMA with LDS DMA)"; }
+const char* tik_version(void) { return "tik 0.4.0 (gfx950; bf16x3 split MFMA (default, fp32 range), exact fp32 MFMA)"; }
 
 int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out) {
     if (!tensors || n_tensors <= 0 || !out) return fail(TIK_E_INVALID, "tik_model_create: null argument");
@@ -965,7 +605,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if (!W0 && !B0 && !W3 && !B3) {
         // backbone-only handle (StgGcn18 state dict, st_gcn_aaai18.py:32-133):
         // tik_backbone_forward only; tik_ik_forward refuses it
-        if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0))) || (rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
+        if ((rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
             delete md;
             return rc;
         }
@@ -979,16 +619,12 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
     md->prec = default_precision();
-    if ((rc = md->zeros.upload(std::vector<unsigned short>(64, 0))) || (rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
+    if ((rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
         delete md;
         return rc;
     }
     apply_env(md);
     if ((rc = md->w0.upload(W0->v)) || (rc = md->b0.upload(B0->v)) || (rc = md->w3.upload(W3->v)) || (rc = md->b3.upload(B3->v)) ||
-        (rc = md->sw0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
-        (rc = md->sw3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
-        (rc = md->sb0.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
-        (rc = md->sb3.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden)) ||
         (rc = md->s30.build(W0->v, md->hidden, 1, md->feat, md->feat)) ||
         (rc = md->s33.build(W3->v, md->pose_dim, 1, md->hidden, md->hidden))) {
         delete md;
@@ -1015,7 +651,15 @@ int tik_model_out_frames(tik_model_t m, int T) {
 
 }  // extern "C"
 
+static bool use_xblk(const tik_model* m);
+
 namespace tik_host {
+// Bytes per pixel (frame x joint) of block 0's output when blocks 0 and 1 run
+// whole (xblock.hip): 64 channels as three bf16 planes, written into the z
+// workspace (blocks01_x), so z must hold N*T*V of them whatever the widths of
+// the later layers.
+constexpr size_t XB0_P3_FLOATS = 64 * 3 * 2 / 4;
+
 int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
     const size_t V = m->V;
     size_t zmax = 0, amax = 0;
@@ -1025,10 +669,11 @@ int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
         t = Layer::tout(t, L.stride);
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
+    if (use_xblk(m)) zmax = std::max(zmax, (size_t)N * T * V * XB0_P3_FLOATS);
     int rc;
     // split-K partials: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
     // (cgemm), or up to 8 K slices of the xgemm head's hidden rows
-    if ((rc = w.xb.reserve((size_t)N * T * V * 32)) || (rc = w.z.reserve(zmax)) || (rc = w.z2.reserve(zmax)) ||
+    if ((rc = w.xb.reserve((size_t)N * T * V * 4)) || (rc = w.z.reserve(zmax)) ||
         (rc = w.a0.reserve(amax)) || (rc = w.a1.reserve(amax)) || (rc = w.hid.reserve((size_t)N * t * m->hidden)) ||
         (rc = w.part.reserve(std::max((size_t)384 * 128 * 128, (size_t)8 * N * t * m->hidden))))
         return rc;
@@ -1072,9 +717,9 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
 }
 
 struct WsPtrs {
-    float *xb, *z, *z2, *a0, *a1, *hid, *part;
+    float *xb, *z, *a0, *a1, *hid, *part;
 };
-static WsPtrs ptrs_of(const Workspace& w) { return WsPtrs{w.xb.p, w.z.p, w.z2.p, w.a0.p, w.a1.p, w.hid.p, w.part.p}; }
+static WsPtrs ptrs_of(const Workspace& w) { return WsPtrs{w.xb.p, w.z.p, w.a0.p, w.a1.p, w.hid.p, w.part.p}; }
 // the workspaces and aux streams of the parts 1 .. np-1 of a split batch
 static int reserve_parts(tik_model* m, int np, int N, int T) {
     int rc;
@@ -1087,27 +732,6 @@ static int reserve_parts(tik_model* m, int np, int N, int T) {
         }
     }
     return TIK_OK;
-}
-
-static bool use_dma(const tik_model* m, int N, int T) {
-    return m->prec == tik::PREC_F16X3 && m->dma_min_frames > 0 && (long long)N * T >= m->dma_min_frames;
-}
-
-// Windows per DMA-path call: the kernels address each activation tensor with
-// 32-bit buffer offsets (out-of-range = zero fill), so every SB tensor of one
-// call must stay below 2 GiB; larger batches run as independent sub-batches.
-static int dma_chunk(const tik_model* m, int T) {
-    long long worst = (long long)T * m->V * 64 * 2;   // layer-0 input block
-    int t = T;
-    for (const Layer& L : m->layers) {
-        const long long row = 64LL * L.sbt.nblk * 2;   // bytes per SB row of cout channels
-        worst = std::max(worst, (long long)t * m->V * row);   // z
-        t = Layer::tout(t, L.stride);
-        worst = std::max(worst, (long long)t * m->V * row);   // out
-    }
-    const long long lim = (1LL << 31) - (1LL << 20);
-    const int c = (int)std::max(1LL, lim / worst);
-    return m->dma_chunk_max > 0 ? std::min(c, m->dma_chunk_max) : c;
 }
 
 // Backbone on fp32 activations (both precisions; split-K for small batches).
@@ -1134,14 +758,15 @@ static int backbone(tik_model_t m, const float* x, int N, int T, float** feat_ou
 }
 
 static bool use_x(const tik_model* m) {
-    if (m->prec != tik::PREC_BF16X3 || !m->xgemm || m->C0 > 4) return false;
+    if (m->prec != tik::PREC_BF16X3 || m->C0 > 4) return false;
     for (const Layer& L : m->layers)
         if (!L.x_ok() || (L.index == 0) != (L.cin <= 4)) return false;
     return true;
 }
 
 // Windows per xgemm call: every fp32 activation tensor the DMA reads stays
-// below 2 GiB (32-bit buffer offsets).
+// below 2 GiB (32-bit buffer offsets), block 0's bf16x3-plane output of the
+// whole-block path included.
 static int x_chunk(const tik_model* m, int T) {
     long long worst = 1;
     int t = T;
@@ -1150,9 +775,10 @@ static int x_chunk(const tik_model* m, int T) {
         t = Layer::tout(t, L.stride);
         worst = std::max(worst, (long long)t * m->V * L.cout * 4);   // out
     }
+    if (use_xblk(m)) worst = std::max(worst, (long long)T * m->V * (long long)(XB0_P3_FLOATS * 4));
     const long long lim = (1LL << 31) - (1LL << 20);
     const int c = (int)std::max(1LL, lim / worst);
-    return m->dma_chunk_max > 0 ? std::min(c, m->dma_chunk_max) : c;
+    return m->x_chunk_max > 0 ? std::min(c, m->x_chunk_max) : c;
 }
 
 // Backbone on fp32 activations with the bf16x3 xgemm kernels. Layer 0 runs
@@ -1247,65 +873,11 @@ static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_
     return TIK_OK;
 }
 
-// Backbone on split-block f16 activations (f16x3, large batches): every
-// layer reads and writes SB rows, operands reach LDS by DMA. Returns the
-// features (SB rows of the last layer) and their row stride.
-static int backbone3(tik_model_t m, const float* x, int N, int T, const half_t** feat_out, int* ld_out, int* tout,
-                     hipStream_t st, const WsPtrs& w) {
-    const int V = m->V;
-    half_t* xs = reinterpret_cast<half_t*>(w.xb);
-    const long long px = (long long)N * T * V;
-    if (!(m->layers.front().raw_ok() && m->layers.front().cin == m->C0)) {
-        ProfScope p("data_bn", 2.0 * px * m->C0, 4.0 * px * (m->C0 + 4), st);
-        HIP_TRY(tik::launch_data_bn_split(x, (int)px, V, m->C0, m->bn_sc.p, m->bn_sh.p, xs, st));
-    }
-    const half_t* cur = xs;
-    int ld = 64, t = T, rc;
-    half_t* bufs[2] = {reinterpret_cast<half_t*>(w.a0), reinterpret_cast<half_t*>(w.a1)};
-    int which = 0;
-    half_t* zb[2] = {reinterpret_cast<half_t*>(w.z), reinterpret_cast<half_t*>(w.z2)};
-    int zi = 0;
-    bool zready = false;
-    for (size_t li = 0; li < m->layers.size(); ++li) {
-        const Layer& L = m->layers[li];
-        half_t* o = bufs[which];
-        const bool raw = li == 0 && L.raw_ok() && L.cin == m->C0;
-        const Layer* nxt = (m->fuse_tg && li + 1 < m->layers.size() && L.can_fuse_next(m->layers[li + 1]))
-                               ? &m->layers[li + 1] : nullptr;
-        if ((rc = L.forward3(cur, ld, N, t, zb[zi], o, m->zeros.p, st, false, raw ? x : nullptr, m->bn_sc.p,
-                             m->bn_sh.p, w.xb, m->stblock, nxt, zb[zi ^ 1], zready, m->tgw ? m->trash.p : nullptr,
-                             m->gpw ? m->trash.p : nullptr)))
-            return rc;
-        zready = nxt != nullptr;
-        if (nxt) zi ^= 1;
-        t = Layer::tout(t, L.stride);
-        cur = o; ld = 64 * L.sbt.nblk; which ^= 1;
-    }
-    *feat_out = cur;
-    *ld_out = ld;
-    *tout = t;
-    return TIK_OK;
-}
-
 int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* feat, void* stream) {
     if (!m || !x || !feat || N <= 0 || T <= 0) return fail(TIK_E_INVALID, "tik_backbone_forward: bad arguments");
     hipStream_t st = (hipStream_t)stream;
     ProfGuard pg(m);
     int to, rc;
-    if (use_dma(m, N, T)) {
-        const int chunk = std::min(N, dma_chunk(m, T));
-        if ((rc = tik_model_reserve(m, chunk, T))) return rc;
-        for (int n0 = 0; n0 < N; n0 += chunk) {
-            const int n = std::min(chunk, N - n0);
-            const half_t* f;
-            int ld;
-            if ((rc = backbone3(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &ld, &to, st, ptrs_of(m->ws[0]))))
-                return rc;
-            const int C = m->layers.back().cout;
-            HIP_TRY(tik::launch_merge(f, (long long)n * to * m->V, C, ld, feat + (size_t)n0 * to * m->feat, st));
-        }
-        return TIK_OK;
-    }
     if (use_x(m)) {
         const int chunk = std::min(N, x_chunk(m, T));
         if ((rc = tik_model_reserve(m, chunk, T))) return rc;
@@ -1325,38 +897,6 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     return TIK_OK;
 }
 
-static int head3(tik_model_t m, const half_t* f, int ldf, int rows, float* poses, hipStream_t st, const WsPtrs& w) {
-    // the features of one frame are its V joint rows back to back: one SB row
-    // of V * ldf halves whose blocks run over (joint, channel) = the reference
-    // flatten order (st_gcn_aaai18.py:131-132)
-    half_t* hs = reinterpret_cast<half_t*>(w.hid);
-    const int ldh = 64 * m->sb3.nblk;
-    tik::Cgemm3Args h{};
-    h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = mkseg3(f, m->V * ldf, m->sb0, 1, 1, 0, rows);
-    h.nseg = 1; h.bias = m->b0.p; h.out_h = hs; h.ldo = ldh;
-    h.act = tik::ACT_LEAKY; h.zeros = m->zeros.p;
-    if (drain_mask() & 4) h.tune |= 2;
-    {
-        ProfScope pr("H3_64x64.head0", 2.0 * rows * m->feat * m->hidden,
-                     4.0 * ((double)rows * (m->feat + m->hidden) + (double)m->feat * m->hidden), st);
-        pr.out(hs, (size_t)rows * ldh * 2);
-        HIP_TRY(tik::launch_cgemm3(h, tik::C3_H64x64, st));
-    }
-    tik::Cgemm3Args p{};
-    p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = mkseg3(hs, ldh, m->sb3, 1, 1, 0, rows);
-    p.nseg = 1; p.bias = m->b3.p; p.out_f = poses; p.ldf = m->pose_dim; p.act = tik::ACT_NONE; p.zeros = m->zeros.p;
-    if (drain_mask() & 4) p.tune |= 2;
-    {
-        ProfScope pr("H3_64x64.head3", 2.0 * rows * m->hidden * m->pose_dim,
-                     4.0 * ((double)rows * (m->hidden + m->pose_dim) + (double)m->hidden * m->pose_dim), st);
-        pr.out(poses, (size_t)rows * m->pose_dim * 4);
-        HIP_TRY(tik::launch_cgemm3(p, tik::C3_H64x64, st));
-    }
-    return TIK_OK;
-}
-
 static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st, int ks = 0);
 
 // Head on fp32 features with split-K (few rows: the K = 4352 loop spread over
@@ -1364,7 +904,7 @@ static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses,
 static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, float* hid, float* part, hipStream_t st) {
     tik::CgemmArgs h{};
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
-    h.seg[0] = mkseg(f, m->w0.p, m->sw0, m->s30, m->feat, m->feat, 1, 1, 0, rows, m->feat);
+    h.seg[0] = mkseg(f, m->w0.p, m->s30, m->feat, m->feat, 1, 1, 0, rows, m->feat);
     h.nseg = 1; h.bias = m->b0.p; h.out = hid; h.ldo = m->hidden; h.act = tik::ACT_LEAKY;
     h.ksplit = tik::splitk_for(h, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
     h.partial = part;
@@ -1381,7 +921,7 @@ static int head_splitk(tik_model_t m, const float* f, int rows, float* poses, fl
 static int head3_splitk(tik_model_t m, const float* hid, int rows, float* poses, float* part, hipStream_t st, int ks) {
     tik::CgemmArgs p{};
     p.M = rows; p.Nc = m->pose_dim; p.V = 1; p.tout = rows;
-    p.seg[0] = mkseg(hid, m->w3.p, m->sw3, m->s33, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
+    p.seg[0] = mkseg(hid, m->w3.p, m->s33, m->hidden, m->hidden, 1, 1, 0, rows, m->hidden);
     p.nseg = 1; p.bias = m->b3.p; p.out = poses; p.ldo = m->pose_dim; p.act = tik::ACT_NONE;
     p.ksplit = ks > 0 ? ks : tik::splitk_for(p, 64, 64, m->prec == tik::PREC_F32 ? 16 : 32, 64);
     p.partial = part;
@@ -1404,7 +944,7 @@ static int head_x(tik_model_t m, const float* f, int rows, float* poses, const W
     h.M = rows; h.Nc = m->hidden; h.V = 1; h.tout = rows;
     h.seg[0] = tik::XSeg{f, m->feat, m->feat, 1, 1, 0, rows, rows};
     h.nseg = 1; h.wp = m->xh0.p; h.ksteps = tik::xgemm_ksteps(h);
-    h.nw = m->layers.front().xnw; h.epi_lds = m->layers.front().xepi != 0;
+    h.nw = 4; h.epi_lds = 1;
     {   // K slices: the fixed count (4: 512 workgroups at 4096 rows), each non-empty
         const int kper = (h.ksteps + m->xhead_ks - 1) / m->xhead_ks;
         h.ksplit = (h.ksteps + kper - 1) / kper;
@@ -1437,51 +977,6 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
                      bool allow_split) {
     float* f;
     int to, rc;
-    if (use_dma(m, N, T)) {
-        const int chunk = std::min(N, dma_chunk(m, T));
-        if ((rc = model_reserve_ws(m, ws, chunk, T))) return rc;
-        // two halves on two streams when the batch is large (not while profiling:
-        // per-launch events would time overlapping kernels)
-        const bool split = allow_split && m->split && !m->profiling && (long long)std::min(N, chunk) * T >= 32768 && N >= 2;
-        const int np = split ? std::min(m->nsplit, std::min(N, chunk)) : 1;
-        if (split && (rc = reserve_parts(m, np, (std::min(N, chunk) + np - 1) / np, T))) return rc;
-        auto half = [&](const float* xs, int n, float* ps, hipStream_t s, const WsPtrs& w) -> int {
-            const half_t* fs;
-            int ld, r;
-            if ((r = backbone3(m, xs, n, T, &fs, &ld, &to, s, w))) return r;
-            if ((long long)n * to <= m->small_head_rows && s == st) {
-                // few rows (online IK): features to fp32 in the free ping-pong buffer, split-K head
-                float* ff = reinterpret_cast<const float*>(fs) == w.a0 ? w.a1 : w.a0;
-                HIP_TRY(tik::launch_merge(fs, (long long)n * to * m->V, m->layers.back().cout, ld, ff, s));
-                return head_splitk(m, ff, n * to, ps, w.hid, w.part, s);
-            }
-            return head3(m, fs, ld, n * to, ps, s, w);
-        };
-        for (int n0 = 0; n0 < N; n0 += chunk) {
-            const int n = std::min(chunk, N - n0);
-            const float* xs = x + (size_t)n0 * T * m->V * m->C0;
-            const int To = tik_model_out_frames(m, T);
-            float* ps = poses + (size_t)n0 * To * m->pose_dim;
-            if (split && n >= np && (long long)n * T >= 32768) {
-                // np parts on np streams (the caller's + handle-owned ones), fork/join by events
-                HIP_TRY(hipEventRecord(m->ev_fork, st));
-                for (int k = 1; k < np; ++k) HIP_TRY(hipStreamWaitEvent(m->aux[k - 1], m->ev_fork, 0));
-                for (int k = 0; k < np; ++k) {
-                    const int a0 = (int)((long long)n * k / np), a1 = (int)((long long)n * (k + 1) / np);
-                    if ((rc = half(xs + (size_t)a0 * T * m->V * m->C0, a1 - a0, ps + (size_t)a0 * To * m->pose_dim,
-                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]))))
-                        return rc;
-                }
-                for (int k = 1; k < np; ++k) {
-                    HIP_TRY(hipEventRecord(m->ev_join[k - 1], m->aux[k - 1]));
-                    HIP_TRY(hipStreamWaitEvent(st, m->ev_join[k - 1], 0));
-                }
-            } else if ((rc = half(xs, n, ps, st, ptrs_of(ws)))) {
-                return rc;
-            }
-        }
-        return TIK_OK;
-    }
     if (use_x(m)) {
         const int chunk = std::min(N, x_chunk(m, T));
         if ((rc = model_reserve_ws(m, ws, chunk, T))) return rc;
@@ -1539,7 +1034,8 @@ int tik_ik_forward(tik_model_t m, const float* x, int N, int T, float* poses, vo
 }
 
 int tik_model_set_precision(tik_model_t m, int prec) {
-    if (!m || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_model_set_precision: bad arguments");
+    if (!m || (prec != tik::PREC_F32 && prec != tik::PREC_BF16X3))
+        return fail(TIK_E_INVALID, "tik_model_set_precision: precision must be 0 (fp32) or 2 (bf16x3), got %d", prec);
     m->prec = prec;
     return TIK_OK;
 }
@@ -1550,7 +1046,8 @@ int tik_model_get_precision(tik_model_t m) {
 }
 
 int tik_block_set_precision(tik_block_t b, int prec) {
-    if (!b || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_block_set_precision: bad arguments");
+    if (!b || (prec != tik::PREC_F32 && prec != tik::PREC_BF16X3))
+        return fail(TIK_E_INVALID, "tik_block_set_precision: precision must be 0 (fp32) or 2 (bf16x3), got %d", prec);
     b->prec = prec;
     return TIK_OK;
 }

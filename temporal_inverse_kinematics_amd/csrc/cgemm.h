@@ -22,17 +22,15 @@ namespace tik {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
 enum { EPI_BIAS = 0, EPI_GRAPH = 1, EPI_SKIN = 2 };
-enum { PREC_F32 = 0, PREC_F16X3 = 1, PREC_BF16X3 = 2 };   // see cgemm.hip
+enum { PREC_F32 = 0, PREC_BF16X3 = 2 };   // see cgemm.hip (1 was the retired f16x3 split)
 
 struct Seg {
     const float* src;   // rows of `ld` floats, cin used (cin % 4 == 0)
     const float* w;     // [Nc][ldw], k = tap*cin + ci                 (PREC_F32)
     int cin, ld, kt, stride, pad, tin, ldw;
-    const unsigned short* whi = nullptr;   // [Nc][ldw8] f16 bits, k = tap*cin8 + ci  (PREC_F16X3)
-    const unsigned short* wlo = nullptr;   // residual w - f16(w), same layout
-    int cin8 = 0, ldw8 = 0;                // cin rounded up to 8; row stride in halves
-    const unsigned short* wb[3] = {nullptr, nullptr, nullptr};   // bf16 planes, w = p0+p1+p2 (PREC_BF16X3),
-                                                                  // layout as whi
+    int cin8 = 0, ldw8 = 0;                // cin rounded up to 8; row stride of the planes in bf16 elements
+    const unsigned short* wb[3] = {nullptr, nullptr, nullptr};   // bf16 planes, w = p0+p1+p2 (PREC_BF16X3):
+                                                                  // [Nc][ldw8], k = tap*cin8 + ci
 };
 
 struct CgemmArgs {

@@ -13,12 +13,10 @@
 //             BK=16; the 4 k of a ds_read_b128 are consumed k-permuted: MFMA
 //             step j takes k = {j, 4+j, 8+j, 12+j} from the 4 lane groups,
 //             identically for A and B, so the sum is unchanged.
-//  PREC_F16X3 v_mfma_f32_16x16x32_f16 on a 2-term split of both operands,
-//             x = x_hi + x_lo (x_hi = f16(x), x_lo = f16(x - x_hi)), fp32
-//             accumulate of  a_lo.b_hi + a_hi.b_lo + a_hi.b_hi  (a_lo.b_lo,
-//             2^-22 relative, dropped): ~fp32 accuracy at 16/3 the f32-MFMA
-//             rate. BK=32. Activations are split when staged into LDS;
-//             weights arrive pre-split (host) as f16 pairs.
+//  PREC_BF16X3 v_mfma_f32_16x16x32_bf16 on x = p0 + p1 + p2 (three bf16
+//             planes, fp32 range), the six products p_i q_j with i + j <= 2,
+//             fp32 accumulation. BK=32. Activations are split when staged into
+//             LDS; weights arrive pre-split (host, SplitW3).
 //
 // Both share the C/D layout (lane holds rows 4*(lane>>4)+e, column lane&15),
 // hence the epilogues.
@@ -27,8 +25,6 @@
 namespace tik {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // column w of the COCO-17 hop<=2 adjacency (Graph('coco','uniform',max_hop=2),
 // mmskeleton/ops/st_gcn/graph.py:76-133): bit v set <=> A[v][w] != 0 (107 entries)
@@ -40,7 +36,6 @@ __host__ __device__ constexpr unsigned coco_hop2_mask(int w) {
 
 template <int PREC> struct PrecCfg;
 template <> struct PrecCfg<PREC_F32> { static constexpr int BK = 16, LDK = 16, ESZ = 4, PLANES = 1; };
-template <> struct PrecCfg<PREC_F16X3> { static constexpr int BK = 32, LDK = 32, ESZ = 2, PLANES = 2; };
 template <> struct PrecCfg<PREC_BF16X3> { static constexpr int BK = 32, LDK = 32, ESZ = 2, PLANES = 3; };
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -91,7 +86,7 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
     constexpr int KQ = BK / 4;
     constexpr int NA4 = BM * KQ;
     constexpr int LA = (NA4 + 255) / 256;
-    // B: F32: BN*KQ float4 slots; F16X3 / BF16X3: BN*(PLANES*BK/8) 16-B slots (one run per plane)
+    // B: F32: BN*KQ float4 slots; BF16X3: BN*(PLANES*BK/8) 16-B slots (one run per plane)
     constexpr int BQ = (PREC == PREC_F32) ? KQ : PC::PLANES * BK / 8;
     constexpr int NB4 = BN * BQ;
     constexpr int LB = (NB4 + 255) / 256;
@@ -160,9 +155,7 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
             bcin_cur = sg.cin8;
 #pragma unroll
             for (int i = 0; i < LB; ++i) {
-                const unsigned short* base;
-                if constexpr (PREC == PREC_F16X3) base = (b_q[i] < 4) ? sg.whi : sg.wlo;
-                else base = (b_q[i] < 4) ? sg.wb[0] : (b_q[i] < 8 ? sg.wb[1] : sg.wb[2]);
+                const unsigned short* base = (b_q[i] < 4) ? sg.wb[0] : (b_q[i] < 8 ? sg.wb[1] : sg.wb[2]);
                 b_ptr[i] = b_live[i] ? reinterpret_cast<const unsigned char*>(
                                            base + (size_t)(n0 + b_lrow[i]) * sg.ldw8 + tap * sg.cin8 + 8 * (b_q[i] & 3))
                                      : nullptr;
@@ -222,32 +215,6 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
             for (int i = 0; i < LB; ++i)
                 if (tid + i * 256 < NB4)
                     *reinterpret_cast<f32x4*>(B0 + (b_q[i] >> 2) * BN * 64 + swz_off(b_lrow[i], b_q[i] & 3)) = rb[i];
-        } else {
-            unsigned char* Ahi = base;
-            unsigned char* Alo = Ahi + BM * 64;
-            unsigned char* Bhi = Alo + BM * 64;
-            unsigned char* Blo = Bhi + BN * 64;
-#pragma unroll
-            for (int i = 0; i < LA; ++i)
-                if (tid + i * 256 < NA4) {
-                    const f32x4 x = ra[i];
-                    f16x4 h, l;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        h[e] = (_Float16)x[e];
-                        l[e] = (_Float16)(x[e] - (float)h[e]);
-                    }
-                    // 4 fp32 channels 4q..4q+3 -> halves 4q..4q+3: chunk q>>1, +8 B when q is odd
-                    const int off = swz_off(a_lrow[i], a_q[i] >> 1) + 8 * (a_q[i] & 1);
-                    *reinterpret_cast<f16x4*>(Ahi + off) = h;
-                    *reinterpret_cast<f16x4*>(Alo + off) = l;
-                }
-#pragma unroll
-            for (int i = 0; i < LB; ++i)
-                if (tid + i * 256 < NB4) {
-                    unsigned char* dst = (b_q[i] < 4) ? Bhi : Blo;
-                    *reinterpret_cast<f32x4*>(dst + swz_off(b_lrow[i], b_q[i] & 3)) = rb[i];
-                }
         }
     };
 
@@ -304,30 +271,6 @@ __global__ __launch_bounds__(256) void cgemm_kernel(CgemmArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0[j], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1[j], acc[i][j], 0, 0, 0);
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[j], acc[i][j], 0, 0, 0);
-                }
-            }
-        } else {
-            const unsigned char* Ahi = base;
-            const unsigned char* Alo = Ahi + BM * 64;
-            const unsigned char* Bhi = Alo + BM * 64;
-            const unsigned char* Blo = Bhi + BN * 64;
-            f16x8 bh[FN], bl[FN];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int off = swz_off(brow + j * 16, g);
-                bh[j] = *reinterpret_cast<const f16x8*>(Bhi + off);
-                bl[j] = *reinterpret_cast<const f16x8*>(Blo + off);
-            }
-#pragma unroll
-            for (int i = 0; i < FM; ++i) {
-                const int off = swz_off(arow + i * 16, g);
-                const f16x8 ah = *reinterpret_cast<const f16x8*>(Ahi + off);
-                const f16x8 al = *reinterpret_cast<const f16x8*>(Alo + off);
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
                 }
             }
         }
@@ -529,12 +472,10 @@ __global__ void splitk_reduce_kernel(CgemmArgs a) {
 template <int BM, int BN, int WM, int WN, int EPI, int VT>
 static hipError_t launch_t(const CgemmArgs& a, int prec, hipStream_t st) {
     const dim3 g((a.M + BM - 1) / BM, (a.Nc + BN - 1) / BN, a.ksplit > 1 ? a.ksplit : 1), blk(256);
-    // the graph tile (BM=272) keeps one staging buffer in f16x3 so that two
+    // the graph tile (BM=272) keeps one staging buffer in bf16x3 so that two
     // workgroups fit a CU's 160 KiB of LDS
     constexpr int NB16 = (EPI == EPI_GRAPH) ? 1 : 2;
-    if (prec == PREC_F16X3)
-        hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F16X3, NB16>), g, blk, 0, st, a);
-    else if (prec == PREC_BF16X3)
+    if (prec == PREC_BF16X3)
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_BF16X3, NB16>), g, blk, 0, st, a);
     else
         hipLaunchKernelGGL((cgemm_kernel<BM, BN, WM, WN, EPI, VT, PREC_F32, 2>), g, blk, 0, st, a);
@@ -568,9 +509,7 @@ int splitk_for(const CgemmArgs& a, int BM, int BN, int bk, int max_split) {
 hipError_t launch_cgemm(const CgemmArgs& a, int cfg, hipStream_t st, int prec) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
     if (a.ksplit > 1 && !a.partial) return hipErrorInvalidValue;
-    if (prec == PREC_F16X3)
-        for (int s = 0; s < a.nseg; ++s)
-            if (!a.seg[s].whi || !a.seg[s].wlo) return hipErrorInvalidValue;
+    if (prec != PREC_F32 && prec != PREC_BF16X3) return hipErrorInvalidValue;
     if (prec == PREC_BF16X3)
         for (int s = 0; s < a.nseg; ++s)
             if (!a.seg[s].wb[0] || !a.seg[s].wb[1] || !a.seg[s].wb[2]) return hipErrorInvalidValue;

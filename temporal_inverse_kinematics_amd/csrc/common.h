@@ -131,31 +131,6 @@ using DevBuf = DevArray<float>;
 using DevIBuf = DevArray<int>;
 using DevHBuf = DevArray<unsigned short>;
 
-// fp32 weights [Nc][kt][cin] (row stride ldw floats) -> f16 hi/lo planes
-// [Nc][kt][cin8] (cin8 = cin rounded up to 8, zero-filled): w = hi + lo with
-// hi = f16(w), lo = f16(w - hi) (round-to-nearest-even both times).
-struct SplitW {
-    DevHBuf hi, lo;
-    int cin8 = 0, ldw8 = 0;
-    int build(const std::vector<float>& w, int Nc, int kt, int cin, int ldw) {
-        cin8 = (cin + 7) & ~7;
-        ldw8 = kt * cin8;
-        std::vector<unsigned short> h((size_t)Nc * ldw8, 0), l((size_t)Nc * ldw8, 0);
-        for (int n = 0; n < Nc; ++n)
-            for (int t = 0; t < kt; ++t)
-                for (int c = 0; c < cin; ++c) {
-                    const float x = w[(size_t)n * ldw + (size_t)t * cin + c];
-                    const _Float16 xh = (_Float16)x;
-                    const _Float16 xl = (_Float16)(x - (float)xh);
-                    h[(size_t)n * ldw8 + (size_t)t * cin8 + c] = __builtin_bit_cast(unsigned short, xh);
-                    l[(size_t)n * ldw8 + (size_t)t * cin8 + c] = __builtin_bit_cast(unsigned short, xl);
-                }
-        int rc;
-        if ((rc = hi.upload(h)) || (rc = lo.upload(l))) return rc;
-        return TIK_OK;
-    }
-};
-
 // fp32 -> bf16 bits, round to nearest even (finite inputs; NaN stays NaN)
 inline unsigned short bf16_rne(float x) {
     unsigned u;
@@ -204,37 +179,12 @@ struct SplitW3 {
     }
 };
 
-// Split-block ("SB") weights for cgemm3.hip: w[n][tap*cin + ci] (row stride
-// ldw floats) -> [Nc][kt][nblk][64] halves, each 32-channel block stored as
-// [hi(w) x32 | lo(w) = f16(w - hi) x32], zero-padded to whole blocks.
-struct SBW {
-    DevHBuf w;
-    int nblk = 0, ldw = 0;
-    int build(const std::vector<float>& src, int Nc, int kt, int cin, int ldw_src) {
-        nblk = (cin + 31) / 32;
-        ldw = kt * nblk * 64;
-        std::vector<unsigned short> h((size_t)Nc * ldw, 0);
-        for (int n = 0; n < Nc; ++n)
-            for (int t = 0; t < kt; ++t)
-                for (int c = 0; c < cin; ++c) {
-                    const float x = src[(size_t)n * ldw_src + (size_t)t * cin + c];
-                    const _Float16 xh = (_Float16)x;
-                    const _Float16 xl = (_Float16)(x - (float)xh);
-                    const size_t o = (size_t)n * ldw + (size_t)t * nblk * 64 + (size_t)(c / 32) * 64 + c % 32;
-                    h[o] = __builtin_bit_cast(unsigned short, xh);
-                    h[o + 32] = __builtin_bit_cast(unsigned short, xl);
-                }
-        return w.upload(h);
-    }
-};
-
 // default arithmetic of the GEMMs (cgemm.h PREC_*): TIK_PRECISION=fp32 the
-// exact f32 MFMA path, =f16x3 the 3-term f16 split (narrower range); default
-// bf16x3, the 6-product bf16 split with fp32's exponent range
+// exact f32 MFMA path; default bf16x3, the 6-product bf16 split with fp32's
+// exponent range
 inline int default_precision() {
     const char* e = getenv("TIK_PRECISION");
     if (e && (std::string(e) == "fp32" || std::string(e) == "f32")) return 0;
-    if (e && std::string(e) == "f16x3") return 1;
     return 2;
 }
 
@@ -243,7 +193,7 @@ inline int default_precision() {
 // online-IK stream owns its own, so a batch call on the handle can never
 // reallocate or overwrite memory a captured stream graph points at.
 struct Workspace {
-    DevBuf xb, z, z2, a0, a1, hid;   // input block, z ping-pong, activation ping-pong, head hidden
+    DevBuf xb, z, a0, a1, hid;       // layer-0 residual input, z, activation ping-pong, head hidden
     DevBuf part;                     // split-K partial sums (small-batch launches)
 };
 

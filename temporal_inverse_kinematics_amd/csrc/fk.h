@@ -17,29 +17,12 @@ struct FkChainArgs {
     float* feat;             // (B,kp)  [vec(R_j - I), j=1..54 | betas | expr | 1 | 0..]  (fp32 GEMM path; or null)
     float* ablk;             // (B,arows,kj) rows e = 4r+c of A_j (3x4), cols j                (fp32 GEMM path; or null)
     int arows;               // rows of ablk per body: 16 (rows 12..15 = [0 0 0 1]) or 12 (the 3x4 part only)
-    unsigned short* feat_sb; // (B, kp/32 blocks of [hi x32 | lo x32]): feat split for the f16x3 GEMM (or null)
-    unsigned short* ablk_sb; // (B*16, kj/32 blocks): ablk split likewise (or null)
     float* ajt;              // (B,55,12) A_j joint-major for the sparse skinning kernel (or null)
     float* joints;           // (B,njoints,3): first 55 written here
     int* dyn_bin;            // (B) or null
     const int* depth;        // (55) depth of each joint in the kinematic tree (root 0)
     int maxdepth;
 };
-
-// Skinning + vertex transform (LBS, smplx lbs.lbs after the blend shapes):
-// verts[b][v] = T[:3,:3] vposed[b][v] + T[:3,3] (+ transl[b]), T = sum_j W[v][j] A_j(b);
-// the T GEMM (rows b*16+e, cols v, K = kj) in f16x3 MFMA on split-block operands.
-struct FkSkinArgs {
-    int B, V, kj;
-    const unsigned short* ablk_sb;   // (B*16, kj) split-block rows
-    const unsigned short* w_sb;      // (V, kj) split-block rows of lbs_weights
-    const float* vposed;             // (B, ldv) v_posed, 3V used
-    int ldv;
-    const float* transl;             // (B,3): a zero array when the caller has none
-    float* verts;                    // (B, 3V)
-    unsigned short* trash;           // >= 1 KB scratch: stores of rows past the batch
-};
-hipError_t launch_fk_skin(const FkSkinArgs& a, hipStream_t st);
 
 // The same LBS on the sparse skinning weights: T = sum over the (at most nz)
 // joints of vertex v with W[v][j] > 2^-30, in ascending joint order, in fp32

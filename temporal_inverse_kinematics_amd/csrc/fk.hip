@@ -12,11 +12,9 @@
 // The two GEMMs (pose/shape blend shapes; skinning + vertex transform) run on
 // the fp32-MFMA implicit-GEMM kernel (cgemm.hip, CFG_T128x128 / CFG_S128x128).
 #include "fk.h"
-#include "cgemm3_dev.h"
+#include "dev_common.h"
 
 namespace tik {
-
-typedef f16x8 f16x8s;
 
 __device__ inline void rodrigues_smplx(float x, float y, float z, float R[9]) {
     // smplx lbs.batch_rodrigues: angle = ||v + 1e-8||, rot_dir = v / angle,
@@ -41,8 +39,6 @@ __device__ inline void rodrigues_smplx(float x, float y, float z, float R[9]) {
 // each joint's G_j from its parent's G_p written at the previous level. The
 // per-element arithmetic is the sequential smplx recursion's, unchanged.
 constexpr int FKW = 4;   // bodies (waves) per workgroup
-
-__device__ __forceinline__ unsigned short f16bits(float x) { return __builtin_bit_cast(unsigned short, (_Float16)x); }
 
 __global__ __launch_bounds__(64 * FKW) void fk_chain_kernel(FkChainArgs a) {
     __shared__ float sG[FKW][55 * 12];
@@ -166,35 +162,9 @@ __global__ __launch_bounds__(64 * FKW) void fk_chain_kernel(FkChainArgs a) {
         o[1] = f32x4{A[4], A[5], A[6], A[7]};
         o[2] = f32x4{A[8], A[9], A[10], A[11]};
     }
-    if (a.ablk_sb) {   // rows b*16+e, K = joint: block j/32, hi at j%32, lo 32 further
-        unsigned short* G = a.ablk_sb + (size_t)b * 16 * (2 * a.kj);
-        for (int e = 0; e < 16; ++e) {
-            const float x = A[e];
-            const _Float16 h = (_Float16)x;
-            const _Float16 l = (_Float16)(x - (float)h);
-            unsigned short* row = G + (size_t)e * 2 * a.kj + (j >> 5) * 64 + (j & 31);
-            row[0] = __builtin_bit_cast(unsigned short, h);
-            row[32] = __builtin_bit_cast(unsigned short, l);
-        }
-    }
     if (a.feat) {
         float* f = a.feat + (size_t)b * a.kp;
         for (int k = j; k < a.kp; k += 64) f[k] = F[k];
-    }
-    if (a.feat_sb) {   // kp/32 blocks of [hi x32 | lo x32]: lane j writes 8 channels of block j/4
-        unsigned short* f = a.feat_sb + (size_t)b * 2 * a.kp;
-        for (int q = j; q < a.kp / 8; q += 64) {
-            const int blk = q >> 2, c0 = (q & 3) * 8;
-            f16x8s hv, lv;
-            for (int e = 0; e < 8; ++e) {
-                const float x = F[blk * 32 + c0 + e];
-                const _Float16 h = (_Float16)x;
-                hv[e] = h;
-                lv[e] = (_Float16)(x - (float)h);
-            }
-            *reinterpret_cast<f16x8s*>(f + blk * 64 + c0) = hv;
-            *reinterpret_cast<f16x8s*>(f + blk * 64 + 32 + c0) = lv;
-        }
     }
 }
 
@@ -233,157 +203,6 @@ __global__ void fk_landmark_kernel(FkLmkArgs a) {
     }
     float* jo = a.joints + ((size_t)b * a.njoints + 55 + k) * 3;
     jo[0] = o[0]; jo[1] = o[1]; jo[2] = o[2];
-}
-
-// Skinning + vertex transform. A workgroup owns 128 vertices (their skinning
-// weights W stay in LDS) and walks a run of body tiles of 8 bodies = 128 rows
-// b*16+e of A (K = 64 joints, 2 split blocks): the next tile's A is DMA'd into
-// the other half of a double buffer and the tile's v_posed rows are loaded
-// into registers before the MFMAs (f16x3, cgemm3's a_lo b_hi + a_hi b_lo +
-// a_hi b_hi). The epilogue works on the accumulators directly: one 16-row
-// fragment is one body, lane group g < 3 holds row g of T_v(b) for vertex
-// lane&15, i.e. output coordinate g, in the order of smplx lbs:
-// T[g,:3] v_posed + T[g,3], then + transl. Every wave issues a fixed number of
-// vector-memory instructions per tile (rows past the batch are clamped on
-// load and redirected to a trash line on store), so the vmcnt waits are exact.
-namespace fks {
-constexpr int BR = 128, BV = 128, IMG = 128 * 128;   // rows (8 bodies x 16), vertices, one block image
-constexpr int NW = 8;                                // waves: 2 (rows) x 4 (vertex columns)
-constexpr int FM = 4, FN = 2;                        // 16x16 fragments per wave
-constexpr int NDA = 2 * 16 / NW;                     // DMA instructions per wave per operand (2 block images x 16)
-constexpr int NLD = FM * FN + FM;                    // loads per wave per tile: v_posed (one dwordx3 per vertex) + transl
-constexpr int NST = FM * FN;                         // vertex stores per wave per tile
-constexpr int SMEM = 2 * IMG + 2 * 2 * IMG;          // W (2 blocks) + A double buffer (2 x 2 blocks): 96 KB
-}  // namespace fks
-
-__global__ __launch_bounds__(512, 1) void fk_skin_kernel(FkSkinArgs a, int runs) {
-    using namespace fks;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int v0 = blockIdx.x * BV;
-    const int nbt = (a.B + 7) / 8;   // body tiles
-    const int t0 = (int)((long long)blockIdx.y * nbt / runs), t1 = (int)((long long)(blockIdx.y + 1) * nbt / runs);
-    const int M = a.B * 16;
-    const i32x4 rA = buf_rsrc(a.ablk_sb, (unsigned)((long long)M * 256));
-    const i32x4 rW = buf_rsrc(a.w_sb, (unsigned)((long long)a.V * 256));
-    static_assert(NDA * NW == 2 * 16, "each operand is 2 block images of 16 DMA instructions");
-    auto dma_img = [&](i32x4 r, int row0, int lim, int blk, unsigned char* img, int rg) {
-        const int rr = rg * 8 + (lane >> 3), ck = (lane & 7) ^ sbf(rr), row = row0 + rr;
-        const unsigned off = row < lim ? (unsigned)((row * 128 + blk * 64 + 8 * ck) * 2) : DMA_OOB;
-        dma16(r, img + rg * 1024, off, 0);
-    };
-    auto issue_a = [&](int t) {   // 2 block images x 16 instructions over 8 waves; t >= t1: zero fill
-        unsigned char* base = smem + 2 * IMG + (t & 1) * 2 * IMG;
-#pragma unroll
-        for (int j = 0; j < NDA; ++j) {
-            const int idx = wave * NDA + j, blk = idx >> 4, rg = idx & 15;
-            dma_img(rA, t * BR, t < t1 ? M : 0, blk, base + blk * IMG, rg);
-        }
-    };
-    // W of this vertex tile, once; then the first A tile
-#pragma unroll
-    for (int j = 0; j < NDA; ++j) {
-        const int idx = wave * NDA + j, blk = idx >> 4, rg = idx & 15;
-        dma_img(rW, v0, a.V, blk, smem + blk * IMG, rg);
-    }
-    const int wm = wave >> 2, wn = wave & 3, g = lane >> 4, l15 = lane & 15;
-    const int gc = g < 3 ? g : 2;   // lane group 3 carries no output row: mirrors row 2, stores to trash
-    float* trash = reinterpret_cast<float*>(a.trash) + (tid & 255);
-    // v_posed rows and translation entries of tile t (rows clamped into the batch): issued one
-    // whole tile ahead, and before that tile's A DMA, so the wait for A(t) also retires them
-    auto load_vp = [&](int t, float (&vp)[FM][FN][3], float (&tb)[FM]) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) tb[i] = a.transl[min(t * 8 + wm * FM + i, a.B - 1) * 3 + gc];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const int body = min(t * 8 + wm * FM + i, a.B - 1);
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int v = min(v0 + wn * 32 + j * 16 + l15, a.V - 1);
-                const float* p = a.vposed + (size_t)body * a.ldv + 3 * v;
-                vp[i][j][0] = p[0]; vp[i][j][1] = p[1]; vp[i][j][2] = p[2];
-            }
-        }
-    };
-    int prev_st = 0;
-    auto step = [&](int t, const float (&vp)[FM][FN][3], const float (&tb)[FM], float (&vpn)[FM][FN][3],
-                    float (&tbn)[FM]) {
-        load_vp(t + 1, vpn, tbn);
-        issue_a(t + 1);
-        // A(t) landed, and with it the older v_posed loads of tile t (younger: the last
-        // tile's stores, tile t+1's loads and A DMA)
-        wait_vm_dyn(prev_st + NLD + NDA);
-        lds_barrier();   // not __syncthreads(): its fence would drain the prefetch (vmcnt(0))
-        const unsigned char* Ab = smem + 2 * IMG + (t & 1) * 2 * IMG;
-        f32x4 acc[FM][FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            const unsigned char* A = Ab + kb * IMG;
-            const unsigned char* Wb = smem + kb * IMG;
-            f16x8 bh[FN], bl[FN];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int r = wn * 32 + j * 16 + l15;
-                bh[j] = *reinterpret_cast<const f16x8*>(Wb + sbo(r, g));
-                bl[j] = *reinterpret_cast<const f16x8*>(Wb + sbo(r, 4 + g));
-            }
-#pragma unroll
-            for (int i = 0; i < FM; ++i) {
-                const int r = wm * 64 + i * 16 + l15;
-                const f16x8 ah = *reinterpret_cast<const f16x8*>(A + sbo(r, g));
-                const f16x8 al = *reinterpret_cast<const f16x8*>(A + sbo(r, 4 + g));
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[j], acc[i][j], 0, 0, 0);
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();   // every wave is done with A(t): its slot takes A(t+2) next tile
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const int body = t * 8 + wm * FM + i;
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int v = v0 + wn * 32 + j * 16 + l15;
-                const f32x4 T = acc[i][j];
-                const float x = fmaf(T[0], vp[i][j][0], fmaf(T[1], vp[i][j][1], fmaf(T[2], vp[i][j][2], T[3])));
-                const bool ok = g < 3 && body < a.B && v < a.V;
-                float* o = ok ? a.verts + (size_t)body * 3 * a.V + 3 * v + g : trash;
-                *o = x + tb[i];
-            }
-        }
-        prev_st = NST;
-    };
-    float vpA[FM][FN][3], tbA[FM], vpB[FM][FN][3], tbB[FM];
-    load_vp(t0, vpA, tbA);
-    issue_a(t0);
-    for (int t = t0; t < t1; t += 2) {   // unrolled by two: the prefetch buffers swap statically
-        step(t, vpA, tbA, vpB, tbB);
-        if (t + 1 < t1) step(t + 1, vpB, tbB, vpA, tbA);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-hipError_t launch_fk_skin(const FkSkinArgs& a, hipStream_t st) {
-    if (a.B <= 0 || a.V <= 0) return hipSuccess;
-    if (a.kj != 64 || !a.ablk_sb || !a.w_sb || !a.vposed || !a.verts || !a.trash || !a.transl || a.ldv < 3 * a.V ||
-        (long long)a.B * 16 * 256 >= (1LL << 31) || (long long)a.B * a.ldv >= (1LL << 31))
-        return hipErrorInvalidValue;
-    const int vt = (a.V + fks::BV - 1) / fks::BV, nbt = (a.B + 7) / 8;
-    // one workgroup per CU (96 KB of LDS) in all, each walking a run of body tiles
-    int runs = 256 / vt > 1 ? 256 / vt : 1;
-    runs = runs < nbt ? runs : nbt;
-    (void)hipGetLastError();
-    hipLaunchKernelGGL(fk_skin_kernel, dim3(vt, runs), dim3(512), 0, st, a, runs);
-    return hipGetLastError();
 }
 
 // Sparse skinning. A workgroup owns 256 consecutive vertices (thread = vertex,

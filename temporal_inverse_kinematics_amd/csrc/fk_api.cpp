@@ -3,12 +3,13 @@
 // and the third-party smplx.SMPLX.forward it calls (lbs + landmarks).
 //
 // Per call (B bodies):
-//   fk_chain            R_j, J, A_j (B,16,64), pose feature (B,512), first 55 joints (wave per body)
-//   tgemm (TG_128x128)  v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
+//   fk_chain            R_j, J, A_j, pose feature (B,512), first 55 joints (wave per body)
+//   fk_blend            v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
 //   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// (f16x3 on split-block operands; bf16x3: both on xgemm.hip, the skinning
-// with its own epilogue EPI_SKIN; fp32 both on cgemm.hip)
+// bf16x3: the blend shapes on xgemm.hip; the skinning on the sparse weights
+// (fk.hip, fp32 FMAs) or, when a vertex has more than 16 live joints, as a
+// GEMM on the persistent xgemm kernel (EPI_SKIN). fp32: both GEMMs on cgemm.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,7 +22,6 @@
 #include "cgemm.h"
 #include "common.h"
 #include "fk.h"
-#include "cgemm3.h"
 #include "xgemm.h"
 
 using namespace tik_host;
@@ -35,18 +35,12 @@ constexpr int KJ = 64;    // padded skinning K (55 joints)
 struct tik_fk {
     int V = 0, F = 0, nb = 0, ne = 0, nlmk = 0, ndyn = 0, nextra = 0, njoints = 0;
     bool contour = false;
-    DevBuf PT;         // [3V][KP]
-    DevBuf WT;         // [V][KJ]
-    SplitW sPT, sWT;   // f16 hi/lo planes (fp32 path's register-staged GEMMs)
-    SplitW3 s3PT, s3WT;   // bf16 planes p0+p1+p2 (bf16x3 register-staged GEMMs)
-    SBW bPT, bWT;      // split-block copies (f16x3: DMA GEMM, skinning kernel)
-    DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM; TIK_FK_XGEMM=0: cgemm.hip)
-    DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the skinning GEMM, EPI_SKIN)
-    bool xpt = true;   // skinning on the persistent xgemm kernel (TIK_FK_PT=0: one workgroup per tile)
-    bool skin12 = true;   // persistent skinning GEMM on the 12 live rows of A_j per body, not 16 (TIK_FK_SKIN12=0: 16)
+    DevBuf PT;         // [3V][KP]    (fp32 path)
+    DevBuf WT;         // [V][KJ]     (fp32 path)
+    DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM)
+    DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the dense skinning GEMM, EPI_SKIN)
     int ncu = 256;
-    int gm = -1;       // blend GEMM row-tile group (XArgs::gm); -1 = auto, one group per XCD (TIK_FK_GM)
-    int prec = 1;
+    int prec = 2;
     // sparse skinning (fk.hip fk_skin_sparse_kernel): per vertex the joints with
     // W > 2^-30 as {joint, weight} pairs, sp_nz per vertex (0: off, TIK_FK_SPARSE=0)
     DevIBuf nzw;
@@ -57,7 +51,7 @@ struct tik_fk {
     int ldv = 0;       // v_posed row stride (3V rounded up to 4 floats: vector stores)
     // workspace
     DevBuf feat, ablk, vposed, verts_ws, ajt;
-    DevHBuf feat_sb, ablk_sb, trash;
+    DevHBuf trash;
     DevBuf zero_transl;   // (B,3) zeros: the skinning kernel always reads a translation
     DevIBuf dyn_bin;
     int cap = 0;
@@ -181,13 +175,10 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         hpm = pm->v;
     }
     fk->prec = default_precision();
-    if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->sPT.build(PT, 3 * V, 1, KP, KP)) ||
-        (rc = fk->sWT.build(WT, V, 1, KJ, KJ)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
+    if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
         (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
         (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||
-        (rc = fk->extra.upload(hex)) || (rc = fk->depth.upload(hdepth)) || (rc = fk->bPT.build(PT, 3 * V, 1, KP, KP)) ||
-        (rc = fk->bWT.build(WT, V, 1, KJ, KJ)) || (rc = fk->s3PT.build(PT, 3 * V, 1, KP, KP)) ||
-        (rc = fk->s3WT.build(WT, V, 1, KJ, KJ))) {
+        (rc = fk->extra.upload(hex)) || (rc = fk->depth.upload(hdepth))) {
         delete fk;
         return rc;
     }
@@ -221,16 +212,12 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
             fk->sp_nz = nz;
         }
     }
-    if (const char* e = getenv("TIK_FK_PT")) fk->xpt = e[0] != '0';
-    if (const char* e = getenv("TIK_FK_SKIN12")) fk->skin12 = e[0] != '0';
-    if (const char* e = getenv("TIK_FK_GM")) fk->gm = atoi(e);
     {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
             fk->ncu = n;
     }
-    const char* xe = getenv("TIK_FK_XGEMM");
-    if (!(xe && xe[0] == '0')) {
+    {
         const tik::XPackSeg ps{PT.data(), KP, 1, KP}, ws{WT.data(), KJ, 1, KJ};
         if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128))) || (rc = fk->xWT.upload(tik::xgemm_pack(&ws, 1, V, 128)))) {
             delete fk;
@@ -251,7 +238,8 @@ int tik_fk_destroy(tik_fk_t fk) {
 }
 
 int tik_fk_set_precision(tik_fk_t fk, int prec) {
-    if (!fk || prec < 0 || prec > 2) return fail(TIK_E_INVALID, "tik_fk_set_precision: bad arguments");
+    if (!fk || (prec != tik::PREC_F32 && prec != tik::PREC_BF16X3))
+        return fail(TIK_E_INVALID, "tik_fk_set_precision: precision must be 0 (fp32) or 2 (bf16x3), got %d", prec);
     fk->prec = prec;
     return TIK_OK;
 }
@@ -271,7 +259,6 @@ int tik_fk_reserve(tik_fk_t fk, int B) {
     if (B <= fk->cap) return TIK_OK;
     int rc;
     if ((rc = fk->feat.reserve((size_t)B * KP)) || (rc = fk->ablk.reserve((size_t)B * 16 * KJ)) ||
-        (rc = fk->feat_sb.reserve((size_t)B * 2 * KP)) || (rc = fk->ablk_sb.reserve((size_t)B * 16 * 2 * KJ)) ||
         (rc = fk->vposed.reserve((size_t)B * fk->ldv)) || (rc = fk->dyn_bin.reserve((size_t)B)) ||
         (fk->sp_nz && (rc = fk->ajt.reserve((size_t)B * 55 * 12))) ||
         (rc = fk->zero_transl.upload(std::vector<float>((size_t)B * 3, 0.f))) ||
@@ -292,18 +279,17 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         if ((rc = fk->verts_ws.reserve((size_t)B * 3 * fk->V))) return rc;
         vout = fk->verts_ws.p;
     }
-    const bool f16x3 = fk->prec == tik::PREC_F16X3;
+    const bool bf = fk->prec == tik::PREC_BF16X3;
     tik::FkChainArgs c{};
     c.B = B; c.nb = fk->nb; c.ne = fk->ne; c.kp = KP; c.kj = KJ; c.njoints = fk->njoints; c.nchain = fk->nchain;
     c.pose = full_pose; c.betas = betas; c.expr = expression; c.transl = transl; c.pose_mean = fk->pose_mean.p;
     c.parents = fk->parents.p; c.chain = fk->chain.p; c.jt = fk->jt.p; c.jd = fk->jd.p;
-    const bool sparse = !f16x3 && fk->sp_nz > 0;
-    c.feat = f16x3 ? nullptr : fk->feat.p; c.ablk = f16x3 || sparse ? nullptr : fk->ablk.p;
+    const bool sparse = bf && fk->sp_nz > 0;
+    c.feat = fk->feat.p; c.ablk = sparse ? nullptr : fk->ablk.p;
     c.ajt = sparse ? fk->ajt.p : nullptr;
-    // rows of A_j per body in ablk: the persistent bf16x3 skinning GEMM skips the [0 0 0 1] row
-    const int ar = fk->prec == tik::PREC_BF16X3 && fk->xWT.p && fk->xpt && fk->skin12 ? 12 : 16;
+    // rows of A_j per body in ablk: the bf16x3 skinning GEMM skips the [0 0 0 1] row
+    const int ar = bf ? 12 : 16;
     c.arows = ar;
-    c.feat_sb = f16x3 ? fk->feat_sb.p : nullptr; c.ablk_sb = f16x3 ? fk->ablk_sb.p : nullptr;
     c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
     c.depth = fk->depth.p; c.maxdepth = fk->maxdepth;
     Profiler* pf = fk->profiling ? &fk->prof : nullptr;
@@ -314,83 +300,64 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     }
 
     const int V3 = 3 * fk->V;
-    if (f16x3) {
-        // v_posed = feat . P on split-block operands (tgemm.hip: LDS-DMA rings, f16x3 MFMA)
-        tik::Cgemm3Args g{};
+    if (bf) {
+        // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA)
+        tik::XArgs g{};
         g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
-        g.seg[0] = tik::Seg3{fk->feat_sb.p, KP / 32, 2 * KP, 1, 1, 0, B, fk->bPT.w.p, fk->bPT.ldw};
-        g.nseg = 1; g.out_f = fk->vposed.p; g.ldf = fk->ldv; g.act = tik::ACT_NONE;
-        HIP_TRY(tik::launch_tgemm(g, tik::TG_128x128, st));
-        // skinning + vertex transform (fk.hip)
-        tik::FkSkinArgs s{};
-        s.B = B; s.V = fk->V; s.kj = KJ; s.ablk_sb = fk->ablk_sb.p; s.w_sb = fk->bWT.w.p;
-        s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
-        s.trash = fk->trash.p;
-        HIP_TRY(tik::launch_fk_skin(s, st));
+        g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
+        g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
+        g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
+        // P^T (V3 x 512 bf16x3, ~97 MB) is the large operand: group the row tiles so each XCD
+        // streams it about once (its contiguous run of workgroups covers gm row tiles x all columns)
+        { const int gx = (B + 127) / 128; g.gm = (gx + 7) / 8; }
+        // algorithmic: K = 507 live blend-shape columns (486 pose + 20 shape + template);
+        // bytes: feat rows in, v_posed out, P^T once
+        ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
+        HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, st));
     } else {
-        if (fk->prec == tik::PREC_BF16X3 && fk->xPT.p) {
-            // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA)
-            tik::XArgs g{};
-            g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
-            g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
-            g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
-            g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
-            // P^T (V3 x 512 bf16x3, ~97 MB) is the large operand: group the row tiles so each XCD
-            // streams it about once (its contiguous run of workgroups covers gm row tiles x all columns)
-            { const int gx = (B + 127) / 128; g.gm = fk->gm >= 0 ? fk->gm : (gx + 7) / 8; }
-            // algorithmic: K = 507 live blend-shape columns (486 pose + 20 shape + template);
-            // bytes: feat rows in, v_posed out, P^T once
-            ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
-            HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, st));
-        } else {
-        tik::CgemmArgs g{};   // v_posed = feat . P
+        tik::CgemmArgs g{};   // v_posed = feat . P (exact fp32 MFMA)
         g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
         g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
-        g.seg[0].whi = fk->sPT.hi.p; g.seg[0].wlo = fk->sPT.lo.p; g.seg[0].cin8 = fk->sPT.cin8; g.seg[0].ldw8 = fk->sPT.ldw8;
-        for (int i = 0; i < 3; ++i) g.seg[0].wb[i] = fk->s3PT.p[i].p;
         g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
-        HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, fk->prec));
-        }
+        ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
+        HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, tik::PREC_F32));
+    }
 
-        if (sparse) {
-            // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
-            tik::FkSkinSpArgs s{};
-            s.B = B; s.V = fk->V; s.nz = fk->sp_nz; s.ajt = fk->ajt.p;
-            s.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
-            s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
-            s.ncu = fk->ncu;
-            // algorithmic: nz joints x 12 entries + the 3x4 vertex transform per (body, vertex);
-            // bytes: A_j in, v_posed in, vertices out, the pairs once
-            ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
-                         4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + 2.0 * Vd * fk->sp_nz), st);
-            HIP_TRY(tik::launch_fk_skin_sparse(s, st));
-        } else if (fk->prec == tik::PREC_BF16X3 && fk->xWT.p) {
-            // skinning + vertex transform on xgemm.hip (EPI_SKIN)
-            tik::XArgs s{};
-            s.M = B * ar; s.Nc = fk->V; s.V = 1; s.tout = B * ar;
-            s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * ar, (long long)B * ar};
-            s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s); s.skin_rows = ar;
-            s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl; s.act = tik::ACT_NONE;
-            // algorithmic: 12 transform entries x 55 joints per (body, vertex) + the
-            // 3x4 vertex transform; bytes: A_j rows and v_posed in, vertices out, W once
-            ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 12 * NJ + 18.0 * Bd * Vd,
-                         4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
-            if (fk->xpt) {   // persistent: the DMA pipeline runs across tiles (K = 64 is 2 steps per tile)
-                s.bias = transl ? transl : fk->zero_transl.p;
-                s.trash = reinterpret_cast<float*>(fk->trash.p);
-                HIP_TRY(tik::launch_xgemm_pt(s, 128, fk->ncu, st, tik::EPI_SKIN));
-            } else {
-                HIP_TRY(tik::launch_xgemm(s, 128, tik::EPI_SKIN, st));
-            }
-        } else {
-        tik::CgemmArgs s{};   // skinning + vertex transform
+    if (sparse) {
+        // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
+        tik::FkSkinSpArgs s{};
+        s.B = B; s.V = fk->V; s.nz = fk->sp_nz; s.ajt = fk->ajt.p;
+        s.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
+        s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
+        s.ncu = fk->ncu;
+        // algorithmic: nz joints x 12 entries + the 3x4 vertex transform per (body, vertex);
+        // bytes: A_j in, v_posed in, vertices out, the pairs once
+        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
+                     4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + 2.0 * Vd * fk->sp_nz), st);
+        HIP_TRY(tik::launch_fk_skin_sparse(s, st));
+    } else if (bf) {
+        // skinning + vertex transform as a GEMM on the persistent xgemm kernel (EPI_SKIN): the DMA
+        // pipeline runs across tiles (K = 64 is 2 steps per tile); rows = body * 12 + transform entry
+        tik::XArgs s{};
+        s.M = B * ar; s.Nc = fk->V; s.V = 1; s.tout = B * ar;
+        s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * ar, (long long)B * ar};
+        s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s); s.skin_rows = ar;
+        s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.act = tik::ACT_NONE;
+        s.bias = transl ? transl : fk->zero_transl.p;
+        s.trash = reinterpret_cast<float*>(fk->trash.p);
+        // algorithmic: 12 transform entries x 55 joints per (body, vertex) + the
+        // 3x4 vertex transform; bytes: A_j rows and v_posed in, vertices out, W once
+        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 12 * NJ + 18.0 * Bd * Vd,
+                     4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
+        HIP_TRY(tik::launch_xgemm_pt(s, 128, fk->ncu, st, tik::EPI_SKIN));
+    } else {
+        tik::CgemmArgs s{};   // skinning + vertex transform (exact fp32 MFMA)
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
         s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
-        s.seg[0].whi = fk->sWT.hi.p; s.seg[0].wlo = fk->sWT.lo.p; s.seg[0].cin8 = fk->sWT.cin8; s.seg[0].ldw8 = fk->sWT.ldw8;
-        for (int i = 0; i < 3; ++i) s.seg[0].wb[i] = fk->s3WT.p[i].p;
         s.nseg = 1; s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl;
-        HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, fk->prec));
-        }
+        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 16 * NJ + 18.0 * Bd * Vd,
+                     4.0 * (Bd * 16 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
+        HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, tik::PREC_F32));
     }
 
     tik::FkLmkArgs l{};

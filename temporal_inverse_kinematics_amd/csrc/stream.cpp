@@ -127,7 +127,7 @@ static int setup_online(tik_stream* s) {
     if ((rc = s->onl_args.upload(std::vector<tik::OnlineArgs>{a}))) return rc;
     // half the CUs: more workgroups only add pollers (measured p50 143 us at 128, 151 us at 256)
     int grid = std::max(1, cu_count() / 2);
-    if (const char* e = getenv("TIK_ONLINE_GRID")) grid = std::max(1, std::min(cu_count(), atoi(e)));
+    if (const char* e = getenv("TIK_ONLINE_GRID")) grid = std::max(1, std::min(cu_count(), atoi(e)));   // test hook
     s->onl_grid = grid;
     s->online = true;
     return TIK_OK;

@@ -84,7 +84,7 @@ hipError_t launch_colstats(const float* A, const float* G, const float* mean, lo
                            int max_chunks, int* nchunk, hipStream_t st, const float* M) {
     if (C % 4) return hipErrorInvalidValue;
     const int gx = (C + 63) / 64;
-    static const int cs_rows = getenv("TIK_CS_ROWS") ? atoi(getenv("TIK_CS_ROWS")) : CS_ROWS;   // A/B knob
+    constexpr int cs_rows = CS_ROWS;   // 128 measured best (256 -5 %, 64 +-0.3 %: profiles/r02_t15_train_ab.txt)
     long long nc = (R + cs_rows - 1) / cs_rows;
     if (nc > max_chunks) nc = max_chunks;
     if (nc < 1) nc = 1;
@@ -518,7 +518,7 @@ hipError_t launch_wgrad(const float* A, int lda, const float* B, int ldb, int M,
     if (M <= 0 || N <= 0) return hipSuccess;
     if (g.C && (g.C % 64 || N != g.kt * g.C || g.V <= 16 || g.tout <= 0)) return hipErrorInvalidValue;
     const int gx = (M + 63) / 64, gy = (N + 63) / 64;
-    static const int target = getenv("TIK_WG_TARGET") ? atoi(getenv("TIK_WG_TARGET")) : 512;   // A/B knob
+    constexpr int target = 512;   // workgroups (256 -3 %, 1024 +-0.3 %: profiles/r02_t15_train_ab.txt)
     long long splits = target / (gx * gy);
     const long long max_by_rows = (R + 255) / 256;   // >= 256 rows per split
     if (splits > max_by_rows) splits = max_by_rows;

@@ -19,6 +19,8 @@
 
 #include <vector>
 
+#include "cgemm.h"   // EPI_*, ACT_*
+
 namespace tik {
 
 struct XSeg {
@@ -91,6 +93,14 @@ int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole fram
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)
 hipError_t launch_xgemm_splitk_reduce(const float* part, int ksplit, int M, int Nc, const float* bias, int act,
                                       float* out, int ldo, hipStream_t st);
+
+// layer 0's spatial half straight from the raw keypoints (layer0.hip; the
+// layered path, TIK_XBLK=0): z = ReLU(mix_A(data_bn(x) . Wg'^T) + bias2) as fp32
+// rows [rows][ldo]; x [rows][C0], C0 <= 4; also writes xb4 = data_bn(x) as
+// [rows][4] fp32 (XArgs::rx, the residual conv's input)
+hipError_t launch_gcn0_f32(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,
+                           const float* wg, int ldwg, const float* bias2, const float* amix, int mix_sparse, int Cout,
+                           float* out, int ldo, float* xb4, hipStream_t st);
 
 // Host packing of the weights of up to two segments (segment s: fp32
 // W_s[n][tap * cin_s + c], row stride ldw_s) into the tile layout above,

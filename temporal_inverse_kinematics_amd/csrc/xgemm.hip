@@ -2,8 +2,8 @@
 //
 // Tile: BM = 32 NW rows x BN columns. Default NW = 4: a 128-row, 256-thread
 // workgroup of <= 80 KB LDS, TWO per CU, so one workgroup's prologue (first
-// DMA round trip) and epilogue run under the other's main loop (NW = 8, one
-// 256-row workgroup per CU: TIK_XNW=8, 9 % slower end to end). Wave w owns
+// DMA round trip) and epilogue run under the other's main loop (one 256-row
+// 8-wave workgroup per CU measured 3-9 % slower; removed). Wave w owns
 // rows 32w..32w+31 (two 16-row fragments) and ALL BN columns, so each A
 // element is read from LDS and split into bf16 planes exactly once per K
 // step, in registers, by the wave that uses it (no split pass, no extra LDS);
@@ -41,7 +41,7 @@
 #include <type_traits>
 
 #include "cgemm.h"
-#include "cgemm3_dev.h"
+#include "dev_common.h"
 #include "common.h"
 #include "xgemm.h"
 #include "xgemm_dev.h"
@@ -1074,11 +1074,11 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.rx && (bn != 64 || epi != EPI_BIAS || a.rxc < 0 || a.rxc > 4)) return hipErrorInvalidValue;
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
-    if (epi == EPI_SKIN && (a.M % 16 || (a.skin_rows && a.skin_rows != 16) || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx || a.nw == 8))
+    if (epi == EPI_SKIN && (a.M % 16 || (a.skin_rows && a.skin_rows != 16) || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx))
         return hipErrorInvalidValue;
     if ((long long)(epi == EPI_SKIN ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
-    const int nw = a.nw == 8 ? 8 : 4, rt = xgemm_tile_rows(epi, nw);
-    if (a.nw != 0 && a.nw != 4 && a.nw != 8) return hipErrorInvalidValue;
+    const int nw = 4, rt = xgemm_tile_rows(epi, nw);
+    if (a.nw != 0 && a.nw != 4) return hipErrorInvalidValue;
     const int ks = a.ksplit > 1 ? a.ksplit : 1;
     if (ks > 1) {   // one kt-1 segment, raw partials, every slice non-empty
         const int kall = xgemm_kmain(a), kper = (kall + ks - 1) / ks;
@@ -1090,18 +1090,14 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     (void)hipGetLastError();
 #define XL(BN_, EPI_, NW__) hipLaunchKernelGGL((xgemm_kernel<BN_, EPI_, NW__, false>), grid, blk, 0, st, a)
     if (ks > 1) {
-        if (bn == 128 && nw == 4) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 4, true>), grid, blk, 0, st, a);
-        else if (bn == 128) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 8, true>), grid, blk, 0, st, a);
+        if (bn == 128) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 4, true>), grid, blk, 0, st, a);
         else return hipErrorInvalidValue;
     } else if (epi == EPI_SKIN) {
         if (bn == 128) XL(128, EPI_SKIN, 4);
         else XL(64, EPI_SKIN, 4);
-    } else if (nw == 4) {
+    } else {
         if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 4); else XL(128, EPI_GRAPH, 4); }
         else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 4); else XL(64, EPI_GRAPH, 4); }
-    } else {
-        if (bn == 128) { if (epi == EPI_BIAS) XL(128, EPI_BIAS, 8); else XL(128, EPI_GRAPH, 8); }
-        else { if (epi == EPI_BIAS) XL(64, EPI_BIAS, 8); else XL(64, EPI_GRAPH, 8); }
     }
 #undef XL
     return hipGetLastError();

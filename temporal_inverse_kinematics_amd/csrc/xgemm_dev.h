@@ -5,7 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "cgemm.h"
-#include "cgemm3_dev.h"
+#include "dev_common.h"
 #include "xgemm.h"
 
 namespace tik {

@@ -1,6 +1,6 @@
-// xtconv.h — the temporal half of a 128-channel stride-1 ST-GCN block with
+// xtws.h — the temporal half of a 128-channel stride-1 ST-GCN block with
 // identity residual (tcn conv 3x1 + folded BN + residual + ReLU) as one
-// persistent launch with the weights resident in LDS (xtconv.hip).
+// persistent, weight-stationary launch (xtws.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,14 +19,10 @@ struct XTConvArgs {
     int ldo;
     int nts;                     // nontemporal stores
     float* trash;                // >= 4 KB: store target of rows past M (branch-free epilogue)
-    int tune;                    // diagnostic builds (-DTIK_XTUNE) only: bits switch parts off (1 loads, 2 split, 4 MFMAs, 8 stores)
+    int tune;                    // diagnostic builds (-DTIK_XTUNE) only: bits switch parts off (1 loads, 2 split, 4 MFMAs, 8 stores); 0
 };
 
-bool xtconv_ok(const XTConvArgs& a);
-// one 512-thread workgroup per CU (ncu, even), each a column half of a row range
-hipError_t launch_xtconv(const XTConvArgs& a, int ncu, hipStream_t st);
-
-// the same layer on xtws.hip: weight-stationary (weights in VGPRs), 8-frame
+// weight-stationary (weights in VGPRs), 8-frame
 // tiles whose 10-frame halo is split once per K block for all 3 taps
 // (T % 8 == 0; the same packed weights, wp; the accumulation runs (K block,
 // tap): equal to XT128 up to fp32 rounding of that order)

@@ -39,7 +39,7 @@
 #include <type_traits>
 
 #include "xgemm_dev.h"
-#include "xtconv.h"
+#include "xtws.h"
 
 namespace tik {
 

@@ -179,7 +179,7 @@ class StgGcn18(nn.Module):
         self.out_channels = config.layers[-1].out_channels
         self._tik = None
         self._tik_key = None
-        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3" | "f16x3"
+        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3"
 
     def out_frames(self, T: int) -> int:
         for s in self.strides:
@@ -239,7 +239,7 @@ class PoseRegressor(nn.Module):
                                             nn.Linear(512, self.pose_dim))
         self._tik = None
         self._tik_key = None
-        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3" | "f16x3"
+        self.tik_precision = None   # None: library default (bf16x3); "fp32" | "bf16x3"
 
     def tik_handle(self):
         """The libtik model handle for the current weights (rebuilt when they change)."""

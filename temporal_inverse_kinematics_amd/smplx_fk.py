@@ -6,9 +6,8 @@ betas, left_hand_pose, right_hand_pose, transl, ...)` -> `.joints`
 (B,144,3), `.vertices` (B,10475,3); `.faces`, `.batch_size`).
 
 All arithmetic runs in libtik.so (tik_fk_*): the kinematic chain (one wave
-per body), the blend-shape GEMM and the skinning GEMM (bf16x3 split MFMA, fp32 range,
-by default; exact fp32 MFMA with precision="fp32"; the narrower f16x3 split
-on split-block operands with precision="f16x3"), the landmark gather.
+per body), the blend-shape GEMM and the skinning (bf16x3 split MFMA, fp32 range,
+by default; exact fp32 MFMA with precision="fp32"), the landmark gather.
 The fixed `batch_size` of smplx (which forces the reference to zero-pad
 chunks, smpl_util.py:49-56) is kept as an attribute only: any batch runs.
 Model files: SMPLX_{MALE,FEMALE,NEUTRAL}.npz (licensed, not shipped) are read
@@ -104,8 +103,7 @@ class SMPLX:
             _lib.check(lib.tik_fk_set_precision(self._h, _lib.precision_code(precision)))
         # the GEMM arithmetic in use (library default bf16x3 unless TIK_PRECISION says otherwise)
         env = os.environ.get("TIK_PRECISION")
-        self.precision = precision if precision is not None else (
-            "fp32" if env in ("fp32", "f32") else ("f16x3" if env == "f16x3" else "bf16x3"))
+        self.precision = precision if precision is not None else ("fp32" if env in ("fp32", "f32") else "bf16x3")
         self.num_joints = _lib.check(lib.tik_fk_num_joints(self._h))
         self.num_verts = _lib.check(lib.tik_fk_num_verts(self._h))
 
@@ -134,6 +132,8 @@ class SMPLX:
             joints, verts = out
             if joints.shape != (B, self.num_joints, 3) or not joints.is_contiguous() or joints.dtype != torch.float32:
                 raise ValueError("out joints must be a contiguous float32 (B, num_joints, 3) tensor")
+            if return_verts and verts is None:
+                raise ValueError("return_verts=True needs an out vertices tensor (out=(joints, verts))")
             if verts is not None and (verts.shape != (B, self.num_verts, 3) or not verts.is_contiguous()
                                       or verts.dtype != torch.float32):
                 raise ValueError("out vertices must be a contiguous float32 (B, num_verts, 3) tensor")

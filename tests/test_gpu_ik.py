@@ -8,22 +8,18 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import f16x3_only, golden, prec_params
+from conftest import golden
 from oracle import stgcn as orc
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.fixture(scope="module", params=prec_params("bf16x3", "bf16x3-xpt", "bf16x3-xnw8", "bf16x3-xepi0", "bf16x3-xepi1",
-                                                   "bf16x3-cgemm", "bf16x3-xchunk", "fp32", "f16x3", "f16x3-dma",
-                                                   "f16x3-reg", "f16x3-dmachunk", "f16x3-layered", "f16x3-nofuse",
-                                                   "f16x3-dmahead"))
+@pytest.fixture(scope="module", params=["bf16x3", "bf16x3-xchunk", "fp32"])
 def model(request):
-    """bf16x3 (the default: 6-product bf16 split, fp32 range); fp32 MFMA;
-    f16x3 with the default GEMM path (split-block activations with
-    LDS DMA at every size, the head as a split-K GEMM on fp32 features when it
-    has few rows); and each f16x3 path forced at every size."""
+    """bf16x3 (the default: 6-product bf16 split, fp32 range), the same in
+    sub-batches of at most 3 windows (the 2 GiB-per-tensor chunking of large
+    batches, exercised at test sizes), and exact fp32 MFMA."""
     import os
     from temporal_inverse_kinematics_amd import _build
     _build.build()
@@ -31,27 +27,7 @@ def model(request):
     prec, _, path = request.param.partition("-")
     m = synthetic_model(win_size=64, device="cuda", precision=prec)
     if path:
-        # "dmachunk": the DMA path with sub-batches of at most 3 windows (the
-        # 2 GiB-per-tensor split of large batches, exercised at test sizes);
-        # "layered": the DMA path with every block as separate G and T kernels
-        # (no whole-block stblock kernel); "nofuse": the DMA path without the next
-        # block's gcn fused into the temporal-conv epilogue (separate G launches);
-        # "dmahead": the DMA path with the split-block head GEMMs at every size
-        env = {"dmachunk": {"TIK_GEMM_PATH": "dma", "TIK_DMA_CHUNK": "3"},
-               "layered": {"TIK_GEMM_PATH": "dma", "TIK_STBLOCK": "0"},
-               "nofuse": {"TIK_GEMM_PATH": "dma", "TIK_FUSE_TG": "0"},
-               "dmahead": {"TIK_GEMM_PATH": "dma", "TIK_SMALL_HEAD": "0"},
-               # bf16x3 on the register-staged cgemm.hip tiles instead of xgemm.hip
-               "cgemm": {"TIK_XGEMM": "0"},
-               # xgemm in sub-batches of at most 3 windows (the 2 GiB-per-tensor split)
-               "xchunk": {"TIK_DMA_CHUNK": "3"},
-               # xgemm with one 256-row, 8-wave workgroup per CU (default: two 128-row ones)
-               "xnw8": {"TIK_XNW": "8"},
-               # xgemm temporal-conv epilogue from registers (half-line stores), and through LDS
-               # with the identity residual as extra K steps (default: loaded in the epilogue)
-               "xepi0": {"TIK_XEPI": "0"}, "xepi1": {"TIK_XEPI": "1"},
-               # temporal convs on the persistent kernel (DMA pipeline across tiles)
-               "xpt": {"TIK_XPT": "255"}}.get(path, {"TIK_GEMM_PATH": path})
+        env = {"xchunk": {"TIK_X_CHUNK": "3"}}[path]
         os.environ.update(env)
         try:
             m.regressor.tik_handle()   # the path is fixed when the handle is created
@@ -120,7 +96,7 @@ def test_run_inference_sample(model):
     assert np.abs(y9 - r["win9"]).max() < TOL
 
 
-@pytest.mark.parametrize("prec", prec_params("bf16x3", "fp32", "f16x3"))
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
 def test_blocks_vs_golden(prec):
     from temporal_inverse_kinematics_amd import synthetic as syn
     from temporal_inverse_kinematics_amd.models import StGcnBlock
@@ -182,25 +158,7 @@ def test_cpu_tensor_refused(model):
         model(torch.zeros(1, 9, 17, 3))
 
 
-@f16x3_only
-def test_model_dma_subbatches_past_2gib(model):
-    """4000 x 64-frame windows: the largest split-block tensor of one call
-    would pass 2 GiB (32-bit buffer offsets), so the DMA path runs two
-    sub-batches; windows on both sides of the split equal their solo solves."""
-    if model.regressor.tik_precision != "f16x3":
-        pytest.skip("the split-block sub-batch split belongs to the f16x3 DMA path")
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    N = 4000
-    x = torch.from_numpy(syn.synthetic_windows(N, 64, seed=5)).cuda()
-    with torch.no_grad():
-        y = model(x)["poses"]
-        pick = [0, 3853, 3854, 3855, 3856, N - 1]
-        solo = torch.cat([model(x[i:i + 1])["poses"] for i in pick])
-    assert torch.isfinite(y).all()
-    assert (y[pick] - solo).abs().max().item() < 2e-5
-
-
-@pytest.mark.parametrize("prec", prec_params("bf16x3", "f16x3"))
+@pytest.mark.parametrize("prec", ["bf16x3"])
 def test_concurrent_streams_bitwise(prec):
     """Four model handles on four HIP streams running concurrently give the
     same poses, bit for bit, as the serial runs (regression: layer 0's graph
@@ -231,36 +189,13 @@ def test_concurrent_streams_bitwise(prec):
                 assert torch.equal(outs[i], ref[i])
 
 
-@f16x3_only
-def test_fused_gcn_epilogue_bitwise():
-    """The next block's gcn fused into the temporal-conv epilogue
-    (TG_128x128_G7) uses the separate G kernel's products and K order: the
-    poses are bit-identical with and without the fusion (1024 x 64 and
-    batches whose last tile is partial)."""
-    import os
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    from temporal_inverse_kinematics_amd.inference import synthetic_model
-    fused = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
-    os.environ["TIK_FUSE_TG"] = "0"
-    try:
-        plain = synthetic_model(win_size=64, device="cuda", precision="f16x3").regressor
-        plain.tik_handle()
-    finally:
-        del os.environ["TIK_FUSE_TG"]
-    for n, T in [(1024, 64), (333, 64), (70, 65)]:
-        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n)).cuda()
-        with torch.no_grad():
-            assert torch.equal(fused(x)["poses"], plain(x)["poses"]), (n, T)
-
-
-@pytest.mark.parametrize("precision,nsplit", [pytest.param("f16x3", 2, marks=f16x3_only), ("bf16x3", 2), ("bf16x3", 3)])
-def test_two_stream_split_bitwise(precision, nsplit):
-    """Large batches run as parts on several HIP streams (a workspace per part,
+def test_two_stream_split_bitwise():
+    """Large batches run as two parts on two HIP streams (a workspace per part,
     fork/join events): poses bit-identical to the one-stream run, including
-    an odd batch and one the DMA sub-batching also splits; bf16x3 also in
-    three parts (TIK_SPLIT_N=3)."""
+    odd batches."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    split = _model_with_env(precision, TIK_SPLIT_N=nsplit)
+    precision = "bf16x3"
+    split = _model_with_env(precision)
     one = _model_with_env(precision, TIK_SPLIT=0)
     for n in (1024, 1001, 513):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 1)).cuda()
@@ -268,9 +203,9 @@ def test_two_stream_split_bitwise(precision, nsplit):
             assert torch.equal(split(x)["poses"], one(x)["poses"]), n
 
 
-def _model_with_env(precision="f16x3", **env):
-    """A model whose handle is built under `env` (the f16x3 split-block DMA
-    kernels' switches by default)."""
+def _model_with_env(precision="bf16x3", **env):
+    """A model whose handle is built under `env` (the switches are read at
+    handle creation)."""
     import os
     from temporal_inverse_kinematics_amd.inference import synthetic_model
     old = {k: os.environ.get(k) for k in env}
@@ -287,15 +222,15 @@ def _model_with_env(precision="f16x3", **env):
     return m
 
 
-@pytest.mark.parametrize("precision", prec_params("bf16x3", "f16x3"))
-def test_two_stream_split_with_dma_chunks_bitwise(precision):
-    """the split interacts with the DMA sub-batching. With
-    TIK_DMA_CHUNK=600 a 1001-window batch runs as a split chunk (600 windows,
+@pytest.mark.parametrize("precision", ["bf16x3"])
+def test_two_stream_split_with_chunks_bitwise(precision):
+    """the split interacts with the sub-batching. With
+    TIK_X_CHUNK=600 a 1001-window batch runs as a split chunk (600 windows,
     two halves) and an unsplit tail chunk (401 windows, below the 32768-frame
     threshold); a 1500-window batch as two split chunks and a 300-window tail.
     Poses are bit-identical to one unchunked stream."""
     from temporal_inverse_kinematics_amd import synthetic as syn
-    chunked = _model_with_env(precision, TIK_DMA_CHUNK=600)
+    chunked = _model_with_env(precision, TIK_X_CHUNK=600)
     one = _model_with_env(precision, TIK_SPLIT=0)
     for n in (1001, 1500):
         x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 7)).cuda()
@@ -303,7 +238,7 @@ def test_two_stream_split_with_dma_chunks_bitwise(precision):
             assert torch.equal(chunked(x)["poses"], one(x)["poses"]), n
 
 
-@pytest.mark.parametrize("precision", prec_params("f16x3", "bf16x3"))
+@pytest.mark.parametrize("precision", ["bf16x3"])
 def test_two_stream_split_repeated_bitwise(precision):
     """the default two-stream split path, repeated 40
     times back to back (the halves overlap differently on every run), stays
@@ -347,48 +282,6 @@ def test_concurrent_streams_layer0_gcn_bitwise():
             torch.cuda.synchronize()
             for i in range(S):
                 assert torch.equal(outs[i], ref[i])
-
-
-@f16x3_only
-def test_weight_stationary_tgw_bitwise():
-    """The stride-1 fused blocks (L3, L4) on the weight-stationary persistent
-    kernel (tgw.hip, TW_128) give poses bit-identical to the TG3 tiles
-    (TIK_TGW=0) and to the layered G + T path (TIK_FUSE_TG=0): same f16x3
-    products in the same K order, same mix order. Batches: the bench size, a
-    ragged one whose last tile is partial, T=65 windows, and a tiny batch with
-    fewer tiles than CUs."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    tgw = _model_with_env(TIK_SPLIT=0)
-    tg3 = _model_with_env(TIK_TGW=0, TIK_SPLIT=0)
-    plain = _model_with_env(TIK_FUSE_TG=0, TIK_SPLIT=0)
-    for n, T in [(1024, 64), (333, 64), (70, 65), (3, 64)]:
-        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 3)).cuda()
-        with torch.no_grad():
-            y = tgw(x)["poses"]
-            assert torch.equal(y, tg3(x)["poses"]), (n, T)
-            assert torch.equal(y, plain(x)["poses"]), (n, T)
-
-
-
-@f16x3_only
-def test_persistent_gcn_gpw_bitwise():
-    """The unfused gcn launches (L2 64->128, L6 128->256, L7 256->256) on the
-    weight-stationary persistent kernel (gpw.hip, GP_*) give poses
-    bit-identical to the G3_272x128 tiles (TIK_GPW=0): same f16x3 products in
-    the same K order, same mix order. With TIK_FUSE_TG=0 every block's gcn goes
-    through it (128->128 is not a gpw shape there, so L3-L5 stay on G3).
-    Batches: the bench size, a ragged one, T=65 windows, fewer tiles than CUs."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    gpw = _model_with_env(TIK_SPLIT=0)
-    g3 = _model_with_env(TIK_GPW=0, TIK_SPLIT=0)
-    gpw_l = _model_with_env(TIK_FUSE_TG=0, TIK_SPLIT=0)
-    g3_l = _model_with_env(TIK_FUSE_TG=0, TIK_GPW=0, TIK_SPLIT=0)
-    for n, T in [(1024, 64), (333, 64), (70, 65), (3, 64), (1, 9)]:
-        x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + 5)).cuda()
-        with torch.no_grad():
-            y = gpw(x)["poses"]
-            assert torch.equal(y, g3(x)["poses"]), (n, T)
-            assert torch.equal(gpw_l(x)["poses"], g3_l(x)["poses"]), (n, T)
 
 
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
@@ -445,41 +338,6 @@ def test_moveai_to_coco_device_bit_exact():
         moveai3d_to_coco_device(torch.zeros(3, 22, 3), k["moveai_names"].tolist())
 
 
-@pytest.mark.parametrize("n", [1024, 37])
-def test_xgemm_head_splitk_matches_cgemm_head(n):
-    """The bf16x3 head (pose_regressor.0 on xgemm with its K loop split over
-    a fixed number of K slices summed in a fixed order) agrees with the
-    register-staged split-K head (TIK_XHEAD_KS=0) to fp32 rounding, and is
-    run-to-run bit-identical."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    xh = _model_with_env("bf16x3", TIK_SPLIT=0)
-    ch = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XHEAD_KS=0)
-    x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 3)).cuda()
-    with torch.no_grad():
-        a = xh(x)["poses"].clone()
-        b = ch(x)["poses"]
-        assert torch.equal(xh(x)["poses"], a)
-    scale = float(b.abs().max())
-    assert float((a - b).abs().max()) <= 2e-6 * max(1.0, scale), float((a - b).abs().max())
-
-
-def test_xgemm_epilogue_variants():
-    """The xgemm temporal-conv epilogues: through LDS (TIK_XEPI=1, default)
-    and through LDS with the identity rows loaded in the epilogue instead of
-    as K steps (2) do the same fp32 operations in the same order ((acc +
-    identity residual) + bias, activation): bit-identical poses. From
-    registers (0) the compiler contracts layer 0's residual-conv terms into
-    FMAs differently: equal to fp32 rounding."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    ms = [_model_with_env("bf16x3", TIK_SPLIT=0, TIK_XEPI=e, TIK_XTWS=0) for e in (0, 1, 2)]
-    for n in (1024, 37):
-        x = torch.from_numpy(syn.synthetic_windows(n, 64, seed=n + 5)).cuda()
-        with torch.no_grad():
-            ys = [m(x)["poses"].clone() for m in ms]
-        assert torch.equal(ys[1], ys[2]), n
-        assert float((ys[0] - ys[1]).abs().max()) < 1e-5, n
-
-
 def test_bf16x3_batch_invariant_bitwise():
     """On the default bf16x3 path every output row is computed with the same
     operations in the same order whatever the batch (row-local GEMM tiles, a
@@ -495,39 +353,6 @@ def test_bf16x3_batch_invariant_bitwise():
         assert torch.equal(part, full[:37])
         for i in (0, 36, 511, 1023):
             assert torch.equal(m(x[i:i + 1])["poses"], full[i:i + 1]), i
-
-
-@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65)])
-def test_xgemm_persistent_bitwise(n, T):
-    """The persistent temporal-conv kernel (TIK_XPT=255: one DMA pipeline across
-    each workgroup's tiles, epilogue operands loaded up front, rows past M
-    stored to a trash line) computes every row with the same operations in the
-    same order as the per-tile kernel: bit-identical poses, including batches
-    whose last tile is partial and batches with fewer tiles than workgroups.
-    (Layer 0's 3-channel residual conv in the epilogue is contracted into FMAs
-    differently by the two kernels, so both sides run it on the persistent
-    kernel: TIK_XPT=1 vs 255.)"""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    pt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=255, TIK_XTWS=0)
-    one = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=1, TIK_XTWS=0)
-    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n + T)).cuda()
-    with torch.no_grad():
-        a = pt(x)["poses"].clone()
-        b = one(x)["poses"]
-    assert torch.equal(a, b), float((a - b).abs().max())
-
-
-def test_xgemm_persistent_layer0_close():
-    """Layer 0 on the persistent kernel vs the per-tile kernel (TIK_XPT=0):
-    equal to fp32 rounding (the 3-channel residual conv is contracted into FMAs
-    differently)."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    pt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=1)
-    one = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XPT=0)
-    x = torch.from_numpy(syn.synthetic_windows(64, 64, seed=9)).cuda()
-    with torch.no_grad():
-        d = float((pt(x)["poses"] - one(x)["poses"]).abs().max())
-    assert d < 1e-5, d
 
 
 @pytest.mark.parametrize("N", [4000, 8192])
@@ -600,26 +425,6 @@ def test_xgraph_vs_tiled(n, T):
     assert torch.equal(a, b), float((a - b).abs().max())
 
 
-@pytest.mark.parametrize("n,T", [(1024, 64), (37, 64), (3, 17), (70, 65), (2, 9), (1, 1), (5, 31)])
-def test_xtconv_vs_tiled(n, T):
-    """The temporal conv of the 128-channel stride-1 blocks as the
-    resident-weight persistent kernel (xtconv.hip: weights in LDS, activations
-    straight into registers; opt-in, TIK_XTC) against the tiled XT128 kernel
-    (TIK_XTC=0, TIK_XTWS=0): the same bf16x3 products in the same K order and the same
-    (acc + x) + bias epilogue, so the poses are bit-identical — at the bench
-    size, partial last row blocks, short windows (taps at both edges), single
-    frames and T=65."""
-    from temporal_inverse_kinematics_amd import synthetic as syn
-    xt = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=255)
-    tl = _model_with_env("bf16x3", TIK_SPLIT=0, TIK_XTC=0, TIK_XTWS=0)
-    x = torch.from_numpy(syn.synthetic_windows(n, T, seed=n * 3 + T)).cuda()
-    with torch.no_grad():
-        a = xt(x)["poses"].clone()
-        b = tl(x)["poses"]
-    assert torch.isfinite(a).all()
-    assert torch.equal(a, b), float((a - b).abs().max())
-
-
 @pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9), (1, 16), (7, 128), (257, 32), (33, 96)])
 def test_xtws_vs_tiled_and_oracle(n, T):
     """The temporal conv of the 128-channel stride-1 blocks (L3, L4) as the
@@ -677,3 +482,49 @@ def test_run_test_end_to_end_and_cli(tmp_path):
     assert p.returncode == 0, p.stderr[-2000:]
     assert "solved 231 frames" in p.stdout
     assert np.array_equal(np.load(dst), out["poses"])
+
+
+@pytest.mark.parametrize("n,T", [(64, 64), (5, 17), (2, 9)])
+def test_xblock_workspace_all_64_channel_backbone(n, T):
+    """with blocks 0 and 1 whole (xblock.hip) block 0's
+    output goes into the z workspace as bf16x3 planes, 384 B per pixel, more
+    than any later 64-channel layer's fp32 z. A backbone of 64-channel layers
+    only (a stride-2 64 -> 64 layer after the two whole blocks) must size z
+    for it: the default path equals the layered one (TIK_XBLK=0) bit for bit
+    and the float64 oracle."""
+    import os
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.models import StgConfig, StgGcn18, StgLayerConfig
+    layers = [(3, 64, 1), (64, 64, 1), (64, 64, 2), (64, 64, 1)]
+    A = orc.graph_A("coco", "uniform", 2, 1)
+    sd = syn.ik_state_dict(A, seed=3, layers=layers)
+    bsd = {k[len("backbone."):]: v for k, v in sd.items() if k.startswith("backbone.")}
+    cfg = StgConfig([StgLayerConfig(a, b, s, True) for a, b, s in layers], 3)
+
+    def make(**env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            m = StgGcn18(cfg, {"layout": "coco", "strategy": "uniform", "max_hop": 2, "dilation": 1})
+            r = m.load_state_dict({k: torch.from_numpy(v) for k, v in bsd.items()}, strict=False)
+            assert not [k for k in r.missing_keys if "num_batches_tracked" not in k] and not r.unexpected_keys, r
+            m = m.cuda().eval()
+            m.tik_handle()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
+        return m
+    xb, lay = make(TIK_SPLIT="0"), make(TIK_SPLIT="0", TIK_XBLK="0")
+    x = syn.synthetic_windows(n, T, seed=n + T)
+    xd = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        a = xb(xd).clone()
+        b = lay(xd)
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).abs().max())
+    ref = orc.backbone(x[:2], sd, layers=layers)
+    assert np.abs(a[:2].cpu().numpy() - ref.reshape(a[:2].shape)).max() < TOL

@@ -160,6 +160,9 @@ def _cpu_child(T: int, seconds: float):
     to the physical cores of one socket BEFORE torch is imported, so the intra-op
     threads never spread over two sockets or SMT siblings."""
     cores = _one_socket_physical_cores()
+    quota = _cgroup_cpus()
+    if quota is not None:   # no more cores than the cgroup's CPU share: threads past it only wait
+        cores = cores[:max(1, int(quota))]
     os.sched_setaffinity(0, cores)
     import numpy as np
     import torch
@@ -169,8 +172,7 @@ def _cpu_child(T: int, seconds: float):
     sd = syn.ik_state_dict(orc.graph_A("coco", "uniform", 2, 1), seed=0)
     nb = 64   # the reference's inference batch (inference.py:43)
     x = syn.synthetic_windows(nb, T, seed=7)
-    quota = _cgroup_cpus()
-    cap = len(cores) if quota is None else max(1, min(len(cores), int(quota)))
+    cap = len(cores)
     cands = [n for n in (8, 16, 32, 64) if n <= cap] or [cap]
     probes = {}
     for n in cands:

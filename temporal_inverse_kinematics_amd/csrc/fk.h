@@ -17,20 +17,20 @@ struct FkChainArgs {
     float* feat;             // (B,kp)  [vec(R_j - I), j=1..54 | betas | expr | 1 | 0..]  (fp32 GEMM path; or null)
     float* ablk;             // (B,arows,kj) rows e = 4r+c of A_j (3x4), cols j                (fp32 GEMM path; or null)
     int arows;               // rows of ablk per body: 16 (rows 12..15 = [0 0 0 1]) or 12 (the 3x4 part only)
-    float* ajt;              // (B,55,12) A_j joint-major for the sparse skinning kernel (or null)
+    float* ajt;              // (55,B,12) A_j joint-major for the sparse / fused skinning (or null)
     float* joints;           // (B,njoints,3): first 55 written here
     int* dyn_bin;            // (B) or null
     const int* depth;        // (55) depth of each joint in the kinematic tree (root 0)
     int maxdepth;
 };
 
-// The same LBS on the sparse skinning weights: T = sum over the (at most nz)
+// LBS on the sparse skinning weights: T = sum over the (at most nz)
 // joints of vertex v with W[v][j] > 2^-30, in ascending joint order, in fp32
 // FMAs (the dense product's terms in its order, minus terms below 2^-30 of a
 // transform); one thread per vertex, a run of bodies per workgroup.
 struct FkSkinSpArgs {
     int B, V, nz;                    // nz: entries per vertex (4, 8 or 16)
-    const float* ajt;                // (B,55,12) A_j, joint-major
+    const float* ajt;                // (55,B,12) A_j, joint-major
     const int2* nzw;                 // (V,nz) {joint, float bits of W[v][joint]}, joints ascending; padding {0, 0}
     const float* vposed;             // (B, ldv) v_posed, 3V used
     int ldv;

@@ -156,8 +156,8 @@ __global__ __launch_bounds__(64 * FKW) void fk_chain_kernel(FkChainArgs a) {
         for (int e = 0; e < ar; ++e)
             if (j < a.kj) G[e * a.kj + j] = A[e];
     }
-    if (a.ajt && j < 55) {   // joint-major: lane j writes its 12 entries
-        f32x4* o = reinterpret_cast<f32x4*>(a.ajt + ((size_t)b * 55 + j) * 12);
+    if (a.ajt && j < 55) {   // joint-major [55][B][12]: lane j writes its 12 entries
+        f32x4* o = reinterpret_cast<f32x4*>(a.ajt + ((size_t)j * a.B + b) * 12);
         o[0] = f32x4{A[0], A[1], A[2], A[3]};
         o[1] = f32x4{A[4], A[5], A[6], A[7]};
         o[2] = f32x4{A[8], A[9], A[10], A[11]};
@@ -239,12 +239,16 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
     }
     f32x4 pa[NA4];
     auto load = [&](int t, float (&pv)[SBT][3]) __attribute__((always_inline)) {   // tile t's A_j and v_posed into registers
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.ajt + (size_t)t * ABUF);
+        // A_j is joint-major in memory ([55][B][12]): slot q = (body, joint, quarter) of the
+        // tile's body-major LDS image reads joint j's 16 B of body t SBT + body
         const int nb = min(SBT, a.B - t * SBT);
 #pragma unroll
         for (int i = 0; i < NA4; ++i) {
             const int q = tid + 256 * i;
-            pa[i] = q < nb * (AB / 4) ? src[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+            const int bb = q / (AB / 4), r = q - bb * (AB / 4), jj = r / 3;
+            pa[i] = q < nb * (AB / 4)
+                        ? *reinterpret_cast<const f32x4*>(a.ajt + ((size_t)jj * a.B + t * SBT + bb) * 12 + 4 * (r - 3 * jj))
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int b = 0; b < SBT; ++b) {

@@ -4,12 +4,16 @@
 //
 // Per call (B bodies):
 //   fk_chain            R_j, J, A_j, pose feature (B,512), first 55 joints (wave per body)
-//   fk_blend            v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
-//   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
+//   fk_blend_skin       v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
+//                       and, in the same launch's epilogue, T_v(b) = sum_j W[v][j] A_j(b),
+//                       verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl): v_posed never leaves the CU
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// bf16x3: the blend shapes on xgemm.hip; the skinning on the sparse weights
-// (fk.hip, fp32 FMAs) or, when a vertex has more than 16 live joints, as a
-// GEMM on the persistent xgemm kernel (EPI_SKIN). fp32: both GEMMs on cgemm.hip.
+// bf16x3 (default): the blend shapes on xgemm.hip with the skinning on the sparse
+// weights (at most 16 live joints per vertex, fp32 FMAs) fused into the epilogue
+// (EPI_LBS). TIK_FK_SKIN=sparse: the same as two launches (fk_blend, then
+// fk.hip's sparse skinning over v_posed in HBM; bitwise-equal vertices), =dense:
+// the skinning as a GEMM on the persistent xgemm kernel (EPI_SKIN; also the path
+// for weights with more than 16 live joints per vertex). fp32: both GEMMs on cgemm.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,12 +41,15 @@ struct tik_fk {
     bool contour = false;
     DevBuf PT;         // [3V][KP]    (fp32 path)
     DevBuf WT;         // [V][KJ]     (fp32 path)
-    DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM)
+    DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM, unfused paths)
+    DevHBuf xPTL;      // the same with the columns permuted per 42-vertex tile ([x | y | z], xgemm_lbs_column): EPI_LBS
+    int ncl = 0;       // columns of the permuted matrix (128 per 42 vertices)
+    int skin = 0;      // skinning path: 0 fused (EPI_LBS), 1 sparse kernel, 2 dense GEMM (TIK_FK_SKIN)
     DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the dense skinning GEMM, EPI_SKIN)
     int ncu = 256;
     int prec = 2;
-    // sparse skinning (fk.hip fk_skin_sparse_kernel): per vertex the joints with
-    // W > 2^-30 as {joint, weight} pairs, sp_nz per vertex (0: off, TIK_FK_SPARSE=0)
+    // sparse skinning (fused, or fk.hip fk_skin_sparse_kernel): per vertex the joints with
+    // W > 2^-30 as {joint, weight} pairs, sp_nz per vertex (0: more than 16, the dense GEMM)
     DevIBuf nzw;
     int sp_nz = 0;
     DevBuf jt, jd, pose_mean, lmk_bary, dyn_bary;
@@ -191,8 +198,9 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
             nzmax = std::max(nzmax, n);
         }
         const int nz = nzmax <= 4 ? 4 : nzmax <= 8 ? 8 : nzmax <= 16 ? 16 : 0;
-        const char* e = getenv("TIK_FK_SPARSE");
-        if (nz && !(e && e[0] == '0')) {
+        const char* e = getenv("TIK_FK_SKIN");   // fused (default) | sparse | dense
+        fk->skin = e && !strcmp(e, "sparse") ? 1 : (e && !strcmp(e, "dense") ? 2 : 0);
+        if (nz && fk->skin != 2) {
             std::vector<int> h((size_t)V * nz * 2, 0);
             for (int v = 0; v < V; ++v) {
                 int n = 0;
@@ -222,6 +230,19 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128))) || (rc = fk->xWT.upload(tik::xgemm_pack(&ws, 1, V, 128)))) {
             delete fk;
             return rc;
+        }
+        if (fk->sp_nz && fk->skin == 0) {   // the permuted blend-shape matrix of the fused path
+            fk->ncl = 128 * ((V + tik::XLBS_VT - 1) / tik::XLBS_VT);
+            std::vector<float> PTL((size_t)fk->ncl * KP, 0.f);
+            for (int n = 0; n < fk->ncl; ++n) {
+                const int r = tik::xgemm_lbs_column(n, V);
+                if (r >= 0) std::memcpy(&PTL[(size_t)n * KP], &PT[(size_t)r * KP], KP * sizeof(float));
+            }
+            const tik::XPackSeg pl{PTL.data(), KP, 1, KP};
+            if ((rc = fk->xPTL.upload(tik::xgemm_pack(&pl, 1, fk->ncl, 128)))) {
+                delete fk;
+                return rc;
+            }
         }
     }
     if (fk->contour && ((rc = fk->dyn_faces.upload(hdf)) || (rc = fk->dyn_bary.upload(db->v)))) {
@@ -300,7 +321,22 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     }
 
     const int V3 = 3 * fk->V;
-    if (bf) {
+    if (sparse && fk->xPTL.p) {
+        // blend shapes + skinning in one launch (xgemm.hip EPI_LBS): v_posed stays on chip
+        tik::XArgs g{};
+        g.M = B; g.Nc = fk->ncl; g.V = 1; g.tout = B;
+        g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
+        g.nseg = 1; g.wp = fk->xPTL.p; g.ksteps = tik::xgemm_ksteps(g);
+        g.out = vout; g.ldo = V3; g.act = tik::ACT_NONE; g.bias = transl ? transl : fk->zero_transl.p;
+        g.lbs_nzw = fk->nzw.p; g.lbs_ajt = fk->ajt.p; g.lbs_nv = fk->V;
+        // the permuted P^T (~98 MB) is the large operand: each XCD streams it about once
+        { const int gx = (B + 127) / 128; g.gm = (gx + 7) / 8; }
+        // algorithmic: the blend GEMM (K = 507 live columns) + nz joints x 12 entries + the 3x4
+        // vertex transform per (body, vertex); bytes: feat rows in, vertices out, P^T and the pairs once
+        ProfRange pr(pf, "fk_blend_skin", 2.0 * Bd * V3 * 507 + 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
+                     4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507 + Bd * 12 * NJ + 2.0 * Vd * fk->sp_nz), st);
+        HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_LBS + fk->sp_nz, st));
+    } else if (bf) {
         // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA)
         tik::XArgs g{};
         g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
@@ -323,7 +359,9 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, tik::PREC_F32));
     }
 
-    if (sparse) {
+    if (sparse && fk->xPTL.p) {
+        // skinned in the blend launch
+    } else if (sparse) {
         // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
         tik::FkSkinSpArgs s{};
         s.B = B; s.V = fk->V; s.nz = fk->sp_nz; s.ajt = fk->ajt.p;

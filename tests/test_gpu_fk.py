@@ -109,12 +109,15 @@ def test_fk_config4_full_batch(consts, model):
 
 @pytest.mark.parametrize("nzmax", [4, 7, 12])
 def test_fk_sparse_skinning(consts, monkeypatch, nzmax):
-    """Skinning on the sparse weights (fk.hip fk_skin_sparse_kernel, the
-    default: per vertex the joints with W > 2^-30, fp32 FMAs in ascending
-    joint order) against the dense skinning GEMM (TIK_FK_SPARSE=0) and the
-    oracle, on weight matrices with up to nzmax live joints per vertex (the 4,
-    8 and 16-entry kernels) plus a tail of tiny nonzero weights below the
-    threshold, at a batch that ends mid body tile; and batch independence."""
+    """Skinning on the sparse weights (per vertex the joints with W > 2^-30,
+    fp32 FMAs in ascending joint order), fused into the blend-shape GEMM's
+    epilogue (the default, xgemm.hip EPI_LBS: v_posed never leaves the CU) and
+    as fk.hip's separate kernel over v_posed in HBM (TIK_FK_SKIN=sparse): the
+    same operations in the same order, so bit-identical vertices; both against
+    the dense skinning GEMM (TIK_FK_SKIN=dense) and the oracle, on weight
+    matrices with up to nzmax live joints per vertex (the 4, 8 and 16-entry
+    kernels) plus a tail of tiny nonzero weights below the threshold, at a
+    batch that ends mid body tile; and batch independence."""
     from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
     c = dict(consts)
     rng = np.random.default_rng(nzmax)
@@ -125,26 +128,50 @@ def test_fk_sparse_skinning(consts, monkeypatch, nzmax):
         idx = rng.choice(55, size=k, replace=False)
         w[v, idx] = rng.uniform(0.05, 1.0, k)
     w /= w.sum(axis=1, keepdims=True)
-    w[w == 0] = 1e-13   # below the threshold: dropped by the sparse kernel
+    w[w == 0] = 1e-13   # below the threshold: dropped by the sparse kernels
     c["lbs_weights"] = w.astype(np.float32)
     B = 37
     pose, betas, expr, transl = _inputs(B, 500 + nzmax)
     cu = lambda a: torch.from_numpy(a).cuda()
     outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("TIK_FK_SPARSE", flag)
+    for flag in ("fused", "sparse", "dense"):
+        monkeypatch.setenv("TIK_FK_SKIN", flag)
         m = SMPLX(c, batch_size=9, precision="bf16x3")
         outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), cu(transl)))
-    (js, vs), (jd, vd) = outs
-    assert torch.isfinite(vs).all()
-    assert float((vs - vd).abs().max()) < 1e-5
-    assert float((js - jd).abs().max()) < 1e-5
+    (jf, vf), (js, vs), (jd, vd) = outs
+    assert torch.isfinite(vf).all()
+    assert torch.equal(vf, vs) and torch.equal(jf, js)
+    assert float((vf - vd).abs().max()) < 1e-5
+    assert float((jf - jd).abs().max()) < 1e-5
     _, vr = sl.smplx_forward(c, pose[[0, 36]], betas[[0, 36]], expr[[0, 36]], transl[[0, 36]])
-    assert np.abs(vs[[0, 36]].cpu().numpy() - vr).max() < TOL
-    monkeypatch.setenv("TIK_FK_SPARSE", "1")
+    assert np.abs(vf[[0, 36]].cpu().numpy() - vr).max() < TOL
+    monkeypatch.setenv("TIK_FK_SKIN", "fused")
     m = SMPLX(c, batch_size=9, precision="bf16x3")
     _, v1 = m.full_forward(cu(pose[36:37]), cu(betas[36:37]), cu(expr[36:37]), cu(transl[36:37]))
-    assert torch.equal(v1, vs[36:37])
+    assert torch.equal(v1, vf[36:37])
+
+
+@pytest.mark.parametrize("B", [1, 129, 1100, 4096])
+def test_fk_fused_lbs_vs_two_launches(consts, monkeypatch, B):
+    """Config #4's default path, the blend shapes with the skinning fused into
+    their epilogue, against the same arithmetic as two launches (TIK_FK_SKIN=
+    sparse): bit-identical vertices and joints at one body, a body tile plus
+    one, a batch whose body tiles do not divide over the XCD groups, and the
+    bench batch; no translation (zeros) at B = 129."""
+    from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
+    pose, betas, expr, transl = _inputs(B, 900 + B)
+    cu = lambda a: torch.from_numpy(a).cuda()
+    tr = None if B == 129 else cu(transl)
+    outs = []
+    for flag in ("fused", "sparse"):
+        monkeypatch.setenv("TIK_FK_SKIN", flag)
+        m = SMPLX(consts, batch_size=9, precision="bf16x3")
+        outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), tr))
+    (jf, vf), (js, vs) = outs
+    assert torch.isfinite(vf).all()
+    assert torch.equal(vf, vs) and torch.equal(jf, js)
+    _, vr = sl.smplx_forward(consts, pose[-1:], betas[-1:], expr[-1:], None if tr is None else transl[-1:])
+    assert np.abs(vf[-1:].cpu().numpy() - vr).max() < TOL
 
 
 def _write_smplx_npz(path, c, components=400):

@@ -22,10 +22,6 @@ namespace tik {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
 enum { EPI_BIAS = 0, EPI_GRAPH = 1, EPI_SKIN = 2 };
-// xgemm.hip only: the FK blend-shape GEMM with the sparse LBS skinning in its
-// epilogue (fk_api.cpp); EPI_LBS + nz, nz = 4, 8 or 16 joints per vertex
-enum { EPI_LBS = 16 };
-__host__ __device__ constexpr int epi_lbs_nz(int epi) { return epi > EPI_LBS ? epi - EPI_LBS : 0; }
 enum { PREC_F32 = 0, PREC_BF16X3 = 2 };   // see cgemm.hip (1 was the retired f16x3 split)
 
 struct Seg {

@@ -30,7 +30,8 @@ struct FkChainArgs {
 // transform); one thread per vertex, a run of bodies per workgroup.
 struct FkSkinSpArgs {
     int B, V, nz;                    // nz: entries per vertex (4, 8 or 16)
-    const float* ajt;                // (55,B,12) A_j, joint-major
+    const float* ajt;                // A_j joint-major: body b, joint j at ajt[(j * ajt_ld + b) * 12]
+    int ajt_ld;                      // bodies per joint row of ajt (>= B: a chunk of a larger batch)
     const int2* nzw;                 // (V,nz) {joint, float bits of W[v][joint]}, joints ascending; padding {0, 0}
     const float* vposed;             // (B, ldv) v_posed, 3V used
     int ldv;

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
             const int q = tid + 256 * i;
             const int bb = q / (AB / 4), r = q - bb * (AB / 4), jj = r / 3;
             pa[i] = q < nb * (AB / 4)
-                        ? *reinterpret_cast<const f32x4*>(a.ajt + ((size_t)jj * a.B + t * SBT + bb) * 12 + 4 * (r - 3 * jj))
+                        ? *reinterpret_cast<const f32x4*>(a.ajt + ((size_t)jj * a.ajt_ld + t * SBT + bb) * 12 + 4 * (r - 3 * jj))
                         : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
@@ -307,7 +307,8 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
 
 hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st) {
     if (a.B <= 0 || a.V <= 0) return hipSuccess;
-    if ((a.nz != 4 && a.nz != 8 && a.nz != 16) || !a.ajt || !a.nzw || !a.vposed || !a.verts || !a.transl || a.ldv < 3 * a.V)
+    if ((a.nz != 4 && a.nz != 8 && a.nz != 16) || !a.ajt || !a.nzw || !a.vposed || !a.verts || !a.transl || a.ldv < 3 * a.V ||
+        a.ajt_ld < a.B)
         return hipErrorInvalidValue;
     constexpr int sbt = 4;   // bodies per tile (8: same time, more VGPRs)
     const int vt = (a.V + 255) / 256, nbt = (a.B + sbt - 1) / sbt;

@@ -4,16 +4,21 @@
 //
 // Per call (B bodies):
 //   fk_chain            R_j, J, A_j, pose feature (B,512), first 55 joints (wave per body)
-//   fk_blend_skin       v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
-//                       and, in the same launch's epilogue, T_v(b) = sum_j W[v][j] A_j(b),
-//                       verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl): v_posed never leaves the CU
+//   fk_blend            v_posed(B,3V) = [vec(R-I) | beta | expr | 1] . [posedirs; shapedirs; exprdirs; v_template]
+//   fk_skin             T_v(b) = sum_j W[v][j] A_j(b); verts = T_v[:3,:3] v_posed + T_v[:,3] (+ transl)
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
-// bf16x3 (default): the blend shapes on xgemm.hip with the skinning on the sparse
-// weights (at most 16 live joints per vertex, fp32 FMAs) fused into the epilogue
-// (EPI_LBS). TIK_FK_SKIN=sparse: the same as two launches (fk_blend, then
-// fk.hip's sparse skinning over v_posed in HBM; bitwise-equal vertices), =dense:
-// the skinning as a GEMM on the persistent xgemm kernel (EPI_SKIN; also the path
-// for weights with more than 16 live joints per vertex). fp32: both GEMMs on cgemm.hip.
+// bf16x3 (default): the blend shapes on xgemm.hip, the skinning on the sparse
+// weights (fk.hip, at most 16 live joints per vertex, fp32 FMAs). Batches of
+// more than one chunk (1024 bodies) run blend + skin per chunk, the chunks
+// alternating between the caller's stream and a handle-owned one, so one
+// chunk's HBM-bound skinning runs beside the next chunk's MFMA-bound blend
+// shapes and v_posed (one chunk: 129 MB) can stay in the Infinity Cache.
+// TIK_FK_SKIN=dense: the skinning as a GEMM on the persistent xgemm kernel
+// (EPI_SKIN; also the path for weights with more than 16 live joints per
+// vertex). fp32: both GEMMs on cgemm.hip.
+// (Tried and not kept: the sparse skinning fused into the blend GEMM's
+// epilogue, v_posed never in HBM: bitwise equal but 1.31 vs 0.91 ms, the
+// per-tile A_j gather is latency-bound; profiles/r05_fk1_*.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,9 +47,15 @@ struct tik_fk {
     DevBuf PT;         // [3V][KP]    (fp32 path)
     DevBuf WT;         // [V][KJ]     (fp32 path)
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM, unfused paths)
-    DevHBuf xPTL;      // the same with the columns permuted per 42-vertex tile ([x | y | z], xgemm_lbs_column): EPI_LBS
-    int ncl = 0;       // columns of the permuted matrix (128 per 42 vertices)
-    int skin = 0;      // skinning path: 0 fused (EPI_LBS), 1 sparse kernel, 2 dense GEMM (TIK_FK_SKIN)
+    bool dense = false;   // TIK_FK_SKIN=dense: the skinning GEMM even when the weights are sparse
+    static constexpr int CHUNK = 1024;   // bodies per blend + skin chunk
+    hipStream_t aux = nullptr;           // the second stream of the chunk pipeline
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    ~tik_fk() {
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (aux) (void)hipStreamDestroy(aux);
+    }
     DevHBuf xWT;       // bf16x3 tiles of W^T for xgemm.hip (the dense skinning GEMM, EPI_SKIN)
     int ncu = 256;
     int prec = 2;
@@ -198,9 +209,9 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
             nzmax = std::max(nzmax, n);
         }
         const int nz = nzmax <= 4 ? 4 : nzmax <= 8 ? 8 : nzmax <= 16 ? 16 : 0;
-        const char* e = getenv("TIK_FK_SKIN");   // fused (default) | sparse | dense
-        fk->skin = e && !strcmp(e, "sparse") ? 1 : (e && !strcmp(e, "dense") ? 2 : 0);
-        if (nz && fk->skin != 2) {
+        const char* e = getenv("TIK_FK_SKIN");   // sparse (default) | dense
+        fk->dense = e && !strcmp(e, "dense");
+        if (nz && !fk->dense) {
             std::vector<int> h((size_t)V * nz * 2, 0);
             for (int v = 0; v < V; ++v) {
                 int n = 0;
@@ -230,19 +241,6 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         if ((rc = fk->xPT.upload(tik::xgemm_pack(&ps, 1, 3 * V, 128))) || (rc = fk->xWT.upload(tik::xgemm_pack(&ws, 1, V, 128)))) {
             delete fk;
             return rc;
-        }
-        if (fk->sp_nz && fk->skin == 0) {   // the permuted blend-shape matrix of the fused path
-            fk->ncl = 128 * ((V + tik::XLBS_VT - 1) / tik::XLBS_VT);
-            std::vector<float> PTL((size_t)fk->ncl * KP, 0.f);
-            for (int n = 0; n < fk->ncl; ++n) {
-                const int r = tik::xgemm_lbs_column(n, V);
-                if (r >= 0) std::memcpy(&PTL[(size_t)n * KP], &PT[(size_t)r * KP], KP * sizeof(float));
-            }
-            const tik::XPackSeg pl{PTL.data(), KP, 1, KP};
-            if ((rc = fk->xPTL.upload(tik::xgemm_pack(&pl, 1, fk->ncl, 128)))) {
-                delete fk;
-                return rc;
-            }
         }
     }
     if (fk->contour && ((rc = fk->dyn_faces.upload(hdf)) || (rc = fk->dyn_bary.upload(db->v)))) {
@@ -314,66 +312,69 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     c.joints = joints; c.dyn_bin = fk->contour ? fk->dyn_bin.p : nullptr;
     c.depth = fk->depth.p; c.maxdepth = fk->maxdepth;
     Profiler* pf = fk->profiling ? &fk->prof : nullptr;
-    const double Bd = B, Vd = fk->V;
+    const double Vd = fk->V;
+    const int V3 = 3 * fk->V;
+    const float* tr = transl ? transl : fk->zero_transl.p;
     {
-        ProfRange pr(pf, "fk_chain", 0.0, 4.0 * Bd * (NJ * 3 + 20 + KP + 16 * KJ), st);
+        ProfRange pr(pf, "fk_chain", 0.0, 4.0 * (double)B * (NJ * 3 + 20 + KP + 16 * KJ), st);
         HIP_TRY(tik::launch_fk_chain(c, st));
     }
 
-    const int V3 = 3 * fk->V;
-    if (sparse && fk->xPTL.p) {
-        // blend shapes + skinning in one launch (xgemm.hip EPI_LBS): v_posed stays on chip
+    // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA), bodies b0 .. b0 + n
+    auto blend = [&](int b0, int n, float* vp, hipStream_t s) -> int {
         tik::XArgs g{};
-        g.M = B; g.Nc = fk->ncl; g.V = 1; g.tout = B;
-        g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
-        g.nseg = 1; g.wp = fk->xPTL.p; g.ksteps = tik::xgemm_ksteps(g);
-        g.out = vout; g.ldo = V3; g.act = tik::ACT_NONE; g.bias = transl ? transl : fk->zero_transl.p;
-        g.lbs_nzw = fk->nzw.p; g.lbs_ajt = fk->ajt.p; g.lbs_nv = fk->V;
-        // the permuted P^T (~98 MB) is the large operand: each XCD streams it about once
-        { const int gx = (B + 127) / 128; g.gm = (gx + 7) / 8; }
-        // algorithmic: the blend GEMM (K = 507 live columns) + nz joints x 12 entries + the 3x4
-        // vertex transform per (body, vertex); bytes: feat rows in, vertices out, P^T and the pairs once
-        ProfRange pr(pf, "fk_blend_skin", 2.0 * Bd * V3 * 507 + 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
-                     4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507 + Bd * 12 * NJ + 2.0 * Vd * fk->sp_nz), st);
-        HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_LBS + fk->sp_nz, st));
-    } else if (bf) {
-        // v_posed = feat . P on xgemm.hip (bf16x3, fp32 feat rows by LDS-DMA)
-        tik::XArgs g{};
-        g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
-        g.seg[0] = tik::XSeg{fk->feat.p, KP, KP, 1, 1, 0, B, B};
+        g.M = n; g.Nc = V3; g.V = 1; g.tout = n;
+        g.seg[0] = tik::XSeg{fk->feat.p + (size_t)b0 * KP, KP, KP, 1, 1, 0, n, n};
         g.nseg = 1; g.wp = fk->xPT.p; g.ksteps = tik::xgemm_ksteps(g);
-        g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
+        g.out = vp; g.ldo = fk->ldv; g.act = tik::ACT_NONE; g.epi_lds = 1;
         // P^T (V3 x 512 bf16x3, ~97 MB) is the large operand: group the row tiles so each XCD
         // streams it about once (its contiguous run of workgroups covers gm row tiles x all columns)
-        { const int gx = (B + 127) / 128; g.gm = (gx + 7) / 8; }
+        { const int gx = (n + 127) / 128; g.gm = (gx + 7) / 8; }
         // algorithmic: K = 507 live blend-shape columns (486 pose + 20 shape + template);
         // bytes: feat rows in, v_posed out, P^T once
-        ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
-        HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, st));
-    } else {
-        tik::CgemmArgs g{};   // v_posed = feat . P (exact fp32 MFMA)
-        g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
-        g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
-        g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
-        ProfRange pr(pf, "fk_blend", 2.0 * Bd * V3 * 507, 4.0 * (Bd * KP + Bd * V3 + (double)V3 * 507), st);
-        HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, tik::PREC_F32));
-    }
-
-    if (sparse && fk->xPTL.p) {
-        // skinned in the blend launch
-    } else if (sparse) {
-        // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
-        tik::FkSkinSpArgs s{};
-        s.B = B; s.V = fk->V; s.nz = fk->sp_nz; s.ajt = fk->ajt.p;
-        s.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
-        s.vposed = fk->vposed.p; s.ldv = fk->ldv; s.transl = transl ? transl : fk->zero_transl.p; s.verts = vout;
-        s.ncu = fk->ncu;
+        ProfRange pr(pf, "fk_blend", 2.0 * n * V3 * 507, 4.0 * ((double)n * KP + (double)n * V3 + (double)V3 * 507), s);
+        HIP_TRY(tik::launch_xgemm(g, 128, tik::EPI_BIAS, s));
+        return TIK_OK;
+    };
+    // skinning + vertex transform on the sparse weights (fk.hip): fp32 FMAs over each vertex's joints
+    auto skin = [&](int b0, int n, const float* vp, hipStream_t s) -> int {
+        tik::FkSkinSpArgs k{};
+        k.B = n; k.V = fk->V; k.nz = fk->sp_nz; k.ajt = fk->ajt.p + (size_t)b0 * 12; k.ajt_ld = B;
+        k.nzw = reinterpret_cast<const int2*>(fk->nzw.p);
+        k.vposed = vp; k.ldv = fk->ldv; k.transl = tr + (size_t)b0 * 3; k.verts = vout + (size_t)b0 * V3;
+        k.ncu = fk->ncu;
         // algorithmic: nz joints x 12 entries + the 3x4 vertex transform per (body, vertex);
         // bytes: A_j in, v_posed in, vertices out, the pairs once
-        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * (12.0 * fk->sp_nz + 9.0),
-                     4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + 2.0 * Vd * fk->sp_nz), st);
-        HIP_TRY(tik::launch_fk_skin_sparse(s, st));
+        ProfRange pr(pf, "fk_skin", 2.0 * n * Vd * (12.0 * fk->sp_nz + 9.0),
+                     4.0 * ((double)n * 12 * NJ + 2.0 * n * V3 + 2.0 * Vd * fk->sp_nz), s);
+        HIP_TRY(tik::launch_fk_skin_sparse(k, s));
+        return TIK_OK;
+    };
+
+    if (sparse) {
+        const int nch = (B + tik_fk::CHUNK - 1) / tik_fk::CHUNK;
+        if (nch > 1 && !fk->aux) {
+            HIP_TRY(hipStreamCreateWithFlags(&fk->aux, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&fk->ev_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&fk->ev_join, hipEventDisableTiming));
+        }
+        if (nch > 1) {
+            HIP_TRY(hipEventRecord(fk->ev_fork, st));
+            HIP_TRY(hipStreamWaitEvent(fk->aux, fk->ev_fork, 0));
+        }
+        for (int k = 0; k < nch; ++k) {
+            const int b0 = k * tik_fk::CHUNK, n = std::min(tik_fk::CHUNK, B - b0);
+            hipStream_t s = (k & 1) ? fk->aux : st;
+            // two v_posed chunk buffers, one per stream (reused in stream order)
+            float* vp = fk->vposed.p + (size_t)(nch > 1 ? (k & 1) * tik_fk::CHUNK : 0) * fk->ldv;
+            if ((rc = blend(b0, n, vp, s)) || (rc = skin(b0, n, vp, s))) return rc;
+        }
+        if (nch > 1) {
+            HIP_TRY(hipEventRecord(fk->ev_join, fk->aux));
+            HIP_TRY(hipStreamWaitEvent(st, fk->ev_join, 0));
+        }
     } else if (bf) {
+        if ((rc = blend(0, B, fk->vposed.p, st))) return rc;
         // skinning + vertex transform as a GEMM on the persistent xgemm kernel (EPI_SKIN): the DMA
         // pipeline runs across tiles (K = 64 is 2 steps per tile); rows = body * 12 + transform entry
         tik::XArgs s{};
@@ -381,20 +382,28 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         s.seg[0] = tik::XSeg{fk->ablk.p, KJ, KJ, 1, 1, 0, B * ar, (long long)B * ar};
         s.nseg = 1; s.wp = fk->xWT.p; s.ksteps = tik::xgemm_ksteps(s); s.skin_rows = ar;
         s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.act = tik::ACT_NONE;
-        s.bias = transl ? transl : fk->zero_transl.p;
+        s.bias = tr;
         s.trash = reinterpret_cast<float*>(fk->trash.p);
         // algorithmic: 12 transform entries x 55 joints per (body, vertex) + the
         // 3x4 vertex transform; bytes: A_j rows and v_posed in, vertices out, W once
-        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 12 * NJ + 18.0 * Bd * Vd,
-                     4.0 * (Bd * 12 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
+        ProfRange pr(pf, "fk_skin", 2.0 * B * Vd * 12 * NJ + 18.0 * B * Vd,
+                     4.0 * ((double)B * 12 * NJ + 2.0 * B * V3 + Vd * NJ), st);
         HIP_TRY(tik::launch_xgemm_pt(s, 128, fk->ncu, st, tik::EPI_SKIN));
     } else {
+        {
+            tik::CgemmArgs g{};   // v_posed = feat . P (exact fp32 MFMA)
+            g.M = B; g.Nc = V3; g.V = 1; g.tout = B;
+            g.seg[0] = tik::Seg{fk->feat.p, fk->PT.p, KP, KP, 1, 1, 0, B, KP};
+            g.nseg = 1; g.out = fk->vposed.p; g.ldo = fk->ldv; g.act = tik::ACT_NONE;
+            ProfRange pr(pf, "fk_blend", 2.0 * B * V3 * 507, 4.0 * ((double)B * KP + (double)B * V3 + (double)V3 * 507), st);
+            HIP_TRY(tik::launch_cgemm(g, tik::CFG_T128x128, st, tik::PREC_F32));
+        }
         tik::CgemmArgs s{};   // skinning + vertex transform (exact fp32 MFMA)
         s.M = B * 16; s.Nc = fk->V; s.V = 1; s.tout = B * 16;
         s.seg[0] = tik::Seg{fk->ablk.p, fk->WT.p, KJ, KJ, 1, 1, 0, B * 16, KJ};
         s.nseg = 1; s.resid = fk->vposed.p; s.ldr = fk->ldv; s.out = vout; s.ldo = V3; s.bias = transl;
-        ProfRange pr(pf, "fk_skin", 2.0 * Bd * Vd * 16 * NJ + 18.0 * Bd * Vd,
-                     4.0 * (Bd * 16 * NJ + 2.0 * Bd * V3 + Vd * NJ), st);
+        ProfRange pr(pf, "fk_skin", 2.0 * B * Vd * 16 * NJ + 18.0 * B * Vd,
+                     4.0 * ((double)B * 16 * NJ + 2.0 * B * V3 + Vd * NJ), st);
         HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, tik::PREC_F32));
     }
 
@@ -404,7 +413,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     l.lmk_bary = fk->lmk_bary.p; l.dyn_faces = fk->dyn_faces.p; l.dyn_bary = fk->dyn_bary.p;
     l.dyn_bin = fk->dyn_bin.p; l.joints = joints;
     {
-        ProfRange pr(pf, "fk_landmarks", 0.0, 4.0 * Bd * (3.0 * 144 + 3.0 * 3 * 3 * 89), st);
+        ProfRange pr(pf, "fk_landmarks", 0.0, 4.0 * (double)B * (3.0 * 144 + 3.0 * 3 * 3 * 89), st);
         HIP_TRY(tik::launch_fk_landmarks(l, st));
     }
     return TIK_OK;

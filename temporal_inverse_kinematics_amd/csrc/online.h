@@ -56,6 +56,7 @@ struct OnlineArgs {
     float* hid;
     float* pose;          // device copy of the pose row
     float* pose_host;     // pinned host copy
+    int* done_host;       // pinned host word: the frame count after this step, written last (the host spins on it)
     // scheduling state: zero at launch, left zero by the last workgroup out
     int* ticket;
     int* done;

@@ -20,6 +20,7 @@
 #include "online.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 using namespace tik_host;
@@ -35,6 +36,7 @@ struct tik_stream {
     DevIBuf count;
     float* host_frame = nullptr;   // pinned
     float* host_pose = nullptr;    // pinned; [pose_dim] = the online kernel's error flag
+    volatile int* host_done = nullptr;   // pinned, coherent: the dataflow kernel's frame count after each step
     long long pushed = 0;
     // the dataflow step (online.hip)
     bool online = false;
@@ -50,6 +52,7 @@ struct tik_stream {
         if (graph) (void)hipGraphDestroy(graph);
         if (host_frame) (void)hipHostFree(host_frame);
         if (host_pose) (void)hipHostFree(host_pose);
+        if (host_done) (void)hipHostFree(const_cast<int*>(host_done));
         if (st) (void)hipStreamDestroy(st);
         if (model) model_release(model);
     }
@@ -118,6 +121,8 @@ static int setup_online(tik_stream* s) {
     a.frame = static_cast<const float*>(dp);
     HIP_TRY(hipHostGetDevicePointer(&dp, s->host_pose, 0));
     a.pose_host = static_cast<float*>(dp);
+    HIP_TRY(hipHostGetDevicePointer(&dp, const_cast<int*>(s->host_done), 0));
+    a.done_host = static_cast<int*>(dp);
     a.trace = nullptr;
     if (const char* e = getenv("TIK_ONLINE_TRACE"); e && e[0] == '1') {
         if ((rc = s->onl_trace.reserve((size_t)8 * task))) return rc;
@@ -170,8 +175,14 @@ int tik_stream_create(tik_model_t model, int win_size, int use_graph, tik_stream
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking)) != hipSuccess) return bail("hipStreamCreate", e);
     if ((e = hipHostMalloc(&s->host_frame, sizeof(float) * s->V * 3, hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
-    if ((e = hipHostMalloc(&s->host_pose, sizeof(float) * (s->pose_dim + 1), hipHostMallocDefault)) != hipSuccess) return bail("hipHostMalloc", e);
+    if ((e = hipHostMalloc(&s->host_pose, sizeof(float) * (s->pose_dim + 1), hipHostMallocCoherent)) != hipSuccess) return bail("hipHostMalloc", e);
     s->host_pose[s->pose_dim] = 0.f;
+    {
+        void* hd = nullptr;
+        if ((e = hipHostMalloc(&hd, sizeof(int), hipHostMallocCoherent)) != hipSuccess) return bail("hipHostMalloc", e);
+        s->host_done = static_cast<volatile int*>(hd);
+        *s->host_done = 0;
+    }
     if ((e = hipMemsetAsync(s->count.p, 0, sizeof(int), s->st)) != hipSuccess) return bail("hipMemset", e);
     if ((e = hipMemsetAsync(s->ring.p, 0, sizeof(float) * s->W * s->V * 3, s->st)) != hipSuccess) return bail("hipMemset", e);
     if ((e = hipStreamSynchronize(s->st)) != hipSuccess) return bail("hipStreamSynchronize", e);
@@ -217,6 +228,7 @@ int tik_stream_reset(tik_stream_t s) {
     if (s->online) HIP_TRY(hipMemsetAsync(s->onl_cnt.p, 0, sizeof(int) * s->onl_cnt.n, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
     s->host_pose[s->pose_dim] = 0.f;
+    *s->host_done = 0;
     s->pushed = 0;
     return TIK_OK;
 }
@@ -239,7 +251,19 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
         int rc = record_step(s);
         if (rc) return rc;
     }
-    HIP_TRY(hipStreamSynchronize(s->st));
+    bool seen = false;
+    if (s->online) {
+        // the dataflow kernel's last workgroup writes the new frame count to pinned
+        // host memory after the pose: spin on it (a few us sooner than the completion
+        // signal hipStreamSynchronize waits for); the stream stays ordered for the next step
+        const int want = (int)((s->pushed + 1) & 0x7fffffff);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (long it = 0;; ++it) {
+            if (*s->host_done == want) { seen = true; break; }
+            if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+        }
+    }
+    if (!seen) HIP_TRY(hipStreamSynchronize(s->st));
     ++s->pushed;   // the step appended the frame to the device ring either way
     if (s->online && s->host_pose[s->pose_dim] != 0.f) {
         s->host_pose[s->pose_dim] = 0.f;

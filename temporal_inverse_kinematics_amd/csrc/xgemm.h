@@ -55,12 +55,6 @@ struct XArgs {
     float* trash;               // xgemm_pt: >= BN floats, the store target of rows past M
     int nts;                    // nontemporal output stores (EPI_BIAS / EPI_GRAPH; the backbone's layer outputs)
     int skin_rows;              // EPI_SKIN on xgemm_pt: GEMM rows per body, 16 (A_j rows 4r+c incl. [0 0 0 1]; 0 = 16) or 12 (3x4 only)
-    // EPI_LBS + nz (the FK blend shapes with the skinning fused, BN 128): rows = bodies,
-    // column tile t = vertices 42t .. 42t + 41 as [x (42) | y (42) | z (42) | 2 zero columns]
-    // (xgemm_lbs_columns); out = verts [M][ldo = 3 V], bias = transl [M][3] (zeros if none)
-    const int* lbs_nzw;         // [V][nz] {joint, float bits of W[v][joint]} pairs, joints ascending (padding {0, 0})
-    const float* lbs_ajt;       // A_j joint-major [55][M][12] (the 3 x 4 part), written by fk_chain
-    int lbs_nv;                 // vertices V
     int ldo;
     int act;
     // split K (EPI_BIAS, one kt-1 segment, no residual, bias or activation):
@@ -95,13 +89,6 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st);
 // epi: EPI_BIAS or EPI_SKIN (bn 128, bias = translations (B,3), zeros if none).
 hipError_t launch_xgemm_pt(const XArgs& a, int bn, int ncu, hipStream_t st, int epi = EPI_BIAS);
 int xgemm_tile_rows(int epi, int nw);   // output rows per workgroup (whole frames for EPI_GRAPH)
-// EPI_LBS: vertices per 128-column tile, and the row of P^T (3V x K, row 3v + c)
-// behind column n of the permuted blend-shape matrix (-1: a zero column)
-constexpr int XLBS_VT = 42;
-inline int xgemm_lbs_column(int n, int V) {
-    const int t = n / 128, c = n % 128, v = XLBS_VT * t + c % XLBS_VT;
-    return c >= 3 * XLBS_VT || v >= V ? -1 : 3 * v + c / XLBS_VT;
-}
 // out[r][c] = act(sum_z part[z][r][c] + bias[c]) for the ksplit partials of a
 // split-K launch (part: [ksplit][M][Nc], fixed summation order: deterministic)
 hipError_t launch_xgemm_splitk_reduce(const float* part, int ksplit, int M, int Nc, const float* bias, int act,

@@ -410,91 +410,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         }
     };
 
-    if constexpr (epi_lbs_nz(EPI) > 0) {
-        // ---- SMPL-X LBS fused into the blend shapes (smplx lbs: v_posed -> T v_posed).
-        // The tile is v_posed of 128 bodies x 42 vertices ([x | y | z] column thirds,
-        // xgemm_lbs_column); it never leaves the CU. Per (body, vertex): T = sum_k
-        // W[v][j_k] A_{j_k}(b) over the vertex's live joints (ascending, fp32 FMAs),
-        // verts = T[:3,:3] v_posed + T[:3,3] + transl: the operations, in the order,
-        // of fk.hip's separate sparse skinning kernel on the same v_posed (bitwise).
-        // A_j is read joint-major ([55][M][12]): a lane group of 4 consecutive
-        // bodies reads 192 contiguous bytes of one joint (3 whole 64-B lines).
-        constexpr int NZ = epi_lbs_nz(EPI), LDC = BN + 4, NVT = XLBS_VT;
-        static_assert(BN == 128 && 3 * NVT <= BN, "LBS tile");
-        float* Cs = reinterpret_cast<float*>(smem);
-        int2* vt = reinterpret_cast<int2*>(smem + BM * LDC * 4);
-        const int v0 = ntile * NVT;
-        const int nvt = min(NVT, a.lbs_nv - v0);
-        constexpr int NVP = (NVT * NZ + NT - 1) / NT;
-        int2 vtr[NVP];
-#pragma unroll
-        for (int u = 0; u < NVP; ++u) {
-            const int q = tid + u * NT;
-            vtr[u] = q < nvt * NZ ? reinterpret_cast<const int2*>(a.lbs_nzw)[(size_t)v0 * NZ + q] : int2{0, 0};
-        }
-        __syncthreads();   // every wave done reading the ring
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-                *reinterpret_cast<f32x4*>(Cs + (wave * RW + 16 * i + (lane & 15)) * LDC + 16 * j + 4 * g) = acc[i][j];
-#pragma unroll
-        for (int u = 0; u < NVP; ++u) {
-            const int q = tid + u * NT;
-            if (q < NVT * NZ) vt[q] = vtr[u];
-        }
-        __syncthreads();
-        // this wave's 32 bodies x the tile's vertices: item = (body quad bq, vertex group vg);
-        // lane = 16 x (body in the quad) + vertex in the group. Per body quad the items of
-        // VU vertex groups are computed (their A_j loads in flight together), then stored
-        const int vl = lane & 15, bl = lane >> 4;
-        const int B = a.M;
-        constexpr int VU = NZ == 4 ? 3 : 1;
-#pragma unroll 1
-        for (int bq = 0; bq < RW / 4; ++bq) {
-            const int lr = wave * RW + 4 * bq + bl, b = r0 + lr;
-            const int bc = b < B ? b : B - 1;
-            const float* crow = Cs + lr * LDC;
-            const float t0 = a.bias[bc * 3], t1 = a.bias[bc * 3 + 1], t2 = a.bias[bc * 3 + 2];
-#pragma unroll 1
-            for (int vg0 = 0; vg0 < 3; vg0 += VU) {
-                float o[VU][3];
-#pragma unroll
-                for (int u = 0; u < VU; ++u) {
-                    const int vloc = 16 * (vg0 + u) + vl, vc = vloc < nvt ? vloc : 0;
-                    const float px = crow[vc], py = crow[NVT + vc], pz = crow[2 * NVT + vc];
-                    float T[12];
-#pragma unroll
-                    for (int e = 0; e < 12; ++e) T[e] = 0.f;
-#pragma unroll
-                    for (int k = 0; k < NZ; ++k) {
-                        const int2 jw = vt[vc * NZ + k];
-                        const float w = __builtin_bit_cast(float, jw.y);
-                        const f32x4* A = reinterpret_cast<const f32x4*>(a.lbs_ajt + ((size_t)jw.x * B + bc) * 12);
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) {
-                            const f32x4 x = A[q];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) T[4 * q + e] = fmaf(w, x[e], T[4 * q + e]);
-                        }
-                    }
-                    o[u][0] = fmaf(T[0], px, fmaf(T[1], py, fmaf(T[2], pz, T[3]))) + t0;
-                    o[u][1] = fmaf(T[4], px, fmaf(T[5], py, fmaf(T[6], pz, T[7]))) + t1;
-                    o[u][2] = fmaf(T[8], px, fmaf(T[9], py, fmaf(T[10], pz, T[11]))) + t2;
-                }
-#pragma unroll
-                for (int u = 0; u < VU; ++u) {
-                    const int vloc = 16 * (vg0 + u) + vl;
-                    if (b < B && vloc < nvt) {
-                        float* dst = a.out + (size_t)b * a.ldo + 3 * (v0 + vloc);
-                        dst[0] = o[u][0];
-                        dst[1] = o[u][1];
-                        dst[2] = o[u][2];
-                    }
-                }
-            }
-        }
-    } else if constexpr (TR) {
+    if constexpr (TR) {
         const float slope = a.act == ACT_RELU ? 0.f : (a.act == ACT_LEAKY ? 0.01f : 1.f);
         float* const outp = SK ? a.out + (size_t)blockIdx.z * a.M * a.ldo : a.out;
         if (a.epi_lds) {
@@ -1142,9 +1058,8 @@ int xgemm_tile_rows(int epi, int nw) {
 
 hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.M <= 0 || a.Nc <= 0) return hipSuccess;
-    const int lnz = epi_lbs_nz(epi);
-    if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH && epi != EPI_SKIN && lnz != 4 && lnz != 8 && lnz != 16) ||
-        !a.wp || !a.out || (epi != EPI_SKIN && !lnz && a.ldo % 4) ||
+    if ((bn != 64 && bn != 128) || (epi != EPI_BIAS && epi != EPI_GRAPH && epi != EPI_SKIN) || !a.wp || !a.out ||
+        (epi != EPI_SKIN && a.ldo % 4) ||
         a.nseg < 1 || a.nseg > 2 || a.ksteps != xgemm_ksteps(a) || xgemm_kmain(a) <= 0)
         return hipErrorInvalidValue;
     for (int s = 0; s <= a.nseg; ++s) {
@@ -1160,9 +1075,6 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (a.idn.src && (a.idn.kt != 1 || a.idn.stride != 1 || a.idn.pad != 0 || a.idn.tin != a.tout || a.idn.cin != a.Nc))
         return hipErrorInvalidValue;
     if (epi == EPI_SKIN && (a.M % 16 || (a.skin_rows && a.skin_rows != 16) || !a.resid || a.ldr < 3 * a.Nc || a.ldo < 3 * a.Nc || a.idn.src || a.rx))
-        return hipErrorInvalidValue;
-    if (lnz && (bn != 128 || !a.lbs_nzw || !a.lbs_ajt || !a.bias || a.lbs_nv <= 0 || a.Nc % 128 ||
-                a.Nc / 128 * XLBS_VT < a.lbs_nv || a.ldo < 3 * a.lbs_nv || a.idn.src || a.rx || a.gm < 0))
         return hipErrorInvalidValue;
     if ((long long)(epi == EPI_SKIN ? a.M / 16 : a.M) * a.ldo >= (1LL << 31) * 1LL * 4) return hipErrorInvalidValue;
     const int nw = 4, rt = xgemm_tile_rows(epi, nw);
@@ -1180,10 +1092,6 @@ hipError_t launch_xgemm(const XArgs& a, int bn, int epi, hipStream_t st) {
     if (ks > 1) {
         if (bn == 128) hipLaunchKernelGGL((xgemm_kernel<128, EPI_BIAS, 4, true>), grid, blk, 0, st, a);
         else return hipErrorInvalidValue;
-    } else if (lnz) {
-        if (lnz == 4) XL(128, EPI_LBS + 4, 4);
-        else if (lnz == 8) XL(128, EPI_LBS + 8, 4);
-        else XL(128, EPI_LBS + 16, 4);
     } else if (epi == EPI_SKIN) {
         if (bn == 128) XL(128, EPI_SKIN, 4);
         else XL(64, EPI_SKIN, 4);

@@ -56,7 +56,7 @@ struct XCfg {
     // <= 80 KB LDS, two per CU, so one workgroup's prologue and epilogue run
     // under the other's main loop
     static constexpr int NW = NW_, NT = 64 * NW, BM = 32 * NW, FM = 2, FN = BN / 16, RW = 32;
-    static constexpr bool TR = EPI == EPI_BIAS || epi_lbs_nz(EPI) > 0;   // transposed MFMA: each lane ends with 4 channels of a row
+    static constexpr bool TR = EPI == EPI_BIAS;   // transposed MFMA: each lane ends with 4 channels of a row
     static constexpr int ABYTES = BM * 128;
     static constexpr int PLANE = BN * 64;
     static constexpr int BBYTES = 3 * PLANE;
@@ -75,9 +75,7 @@ struct XCfg {
     static constexpr int RT = EPI == EPI_GRAPH ? BM / 17 * 17 : BM;   // valid rows per tile (whole frames for the mix)
     static constexpr int LDCG = BN + 4;
     // C tile (+ the bias2 slice for the graph mix)
-    // (EPI_LBS: + the column tile's vertex joint lists, 42 x nz {joint, weight} pairs)
-    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4
-                              : (EPI == EPI_SKIN ? 0 : BM * LDCG * 4 + 42 * epi_lbs_nz(EPI) * 8);
+    static constexpr int CT = EPI == EPI_GRAPH ? BM * LDCG * 4 + 17 * BN * 4 : (EPI == EPI_SKIN ? 0 : BM * LDCG * 4);
     static constexpr int SMEM = RING > CT ? RING : CT;
     static constexpr int WG_PER_CU = NW == 8 ? 1 : 2;
     static_assert(NIA * 1024 * NW == ABYTES && NIA * 8 == RW, "A DMA split");

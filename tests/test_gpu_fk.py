@@ -109,12 +109,9 @@ def test_fk_config4_full_batch(consts, model):
 
 @pytest.mark.parametrize("nzmax", [4, 7, 12])
 def test_fk_sparse_skinning(consts, monkeypatch, nzmax):
-    """Skinning on the sparse weights (per vertex the joints with W > 2^-30,
-    fp32 FMAs in ascending joint order), fused into the blend-shape GEMM's
-    epilogue (the default, xgemm.hip EPI_LBS: v_posed never leaves the CU) and
-    as fk.hip's separate kernel over v_posed in HBM (TIK_FK_SKIN=sparse): the
-    same operations in the same order, so bit-identical vertices; both against
-    the dense skinning GEMM (TIK_FK_SKIN=dense) and the oracle, on weight
+    """Skinning on the sparse weights (fk.hip, the default: per vertex the
+    joints with W > 2^-30, fp32 FMAs in ascending joint order) against the
+    dense skinning GEMM (TIK_FK_SKIN=dense) and the oracle, on weight
     matrices with up to nzmax live joints per vertex (the 4, 8 and 16-entry
     kernels) plus a tail of tiny nonzero weights below the threshold, at a
     batch that ends mid body tile; and batch independence."""
@@ -134,44 +131,41 @@ def test_fk_sparse_skinning(consts, monkeypatch, nzmax):
     pose, betas, expr, transl = _inputs(B, 500 + nzmax)
     cu = lambda a: torch.from_numpy(a).cuda()
     outs = []
-    for flag in ("fused", "sparse", "dense"):
+    for flag in ("sparse", "dense"):
         monkeypatch.setenv("TIK_FK_SKIN", flag)
         m = SMPLX(c, batch_size=9, precision="bf16x3")
         outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), cu(transl)))
-    (jf, vf), (js, vs), (jd, vd) = outs
+    (jf, vf), (jd, vd) = outs
     assert torch.isfinite(vf).all()
-    assert torch.equal(vf, vs) and torch.equal(jf, js)
     assert float((vf - vd).abs().max()) < 1e-5
     assert float((jf - jd).abs().max()) < 1e-5
     _, vr = sl.smplx_forward(c, pose[[0, 36]], betas[[0, 36]], expr[[0, 36]], transl[[0, 36]])
     assert np.abs(vf[[0, 36]].cpu().numpy() - vr).max() < TOL
-    monkeypatch.setenv("TIK_FK_SKIN", "fused")
+    monkeypatch.setenv("TIK_FK_SKIN", "sparse")
     m = SMPLX(c, batch_size=9, precision="bf16x3")
     _, v1 = m.full_forward(cu(pose[36:37]), cu(betas[36:37]), cu(expr[36:37]), cu(transl[36:37]))
     assert torch.equal(v1, vf[36:37])
 
 
-@pytest.mark.parametrize("B", [1, 129, 1100, 4096])
-def test_fk_fused_lbs_vs_two_launches(consts, monkeypatch, B):
-    """Config #4's default path, the blend shapes with the skinning fused into
-    their epilogue, against the same arithmetic as two launches (TIK_FK_SKIN=
-    sparse): bit-identical vertices and joints at one body, a body tile plus
-    one, a batch whose body tiles do not divide over the XCD groups, and the
-    bench batch; no translation (zeros) at B = 129."""
+@pytest.mark.parametrize("B", [1, 1025, 2500, 4096])
+def test_fk_chunk_pipeline_batch_invariant(consts, B):
+    """Batches of more than one 1024-body chunk run blend + skinning per chunk,
+    the chunks alternating between two HIP streams (fk_api.cpp): every body's
+    vertices and joints are bit-identical to the same body solved alone (the
+    chunking only partitions rows), at one body, a chunk plus one, a ragged
+    last chunk and config #4's batch; sampled bodies against the oracle."""
     from temporal_inverse_kinematics_amd.smplx_fk import SMPLX
     pose, betas, expr, transl = _inputs(B, 900 + B)
     cu = lambda a: torch.from_numpy(a).cuda()
-    tr = None if B == 129 else cu(transl)
-    outs = []
-    for flag in ("fused", "sparse"):
-        monkeypatch.setenv("TIK_FK_SKIN", flag)
-        m = SMPLX(consts, batch_size=9, precision="bf16x3")
-        outs.append(m.full_forward(cu(pose), cu(betas), cu(expr), tr))
-    (jf, vf), (js, vs) = outs
-    assert torch.isfinite(vf).all()
-    assert torch.equal(vf, vs) and torch.equal(jf, js)
-    _, vr = sl.smplx_forward(consts, pose[-1:], betas[-1:], expr[-1:], None if tr is None else transl[-1:])
-    assert np.abs(vf[-1:].cpu().numpy() - vr).max() < TOL
+    m = SMPLX(consts, batch_size=9, precision="bf16x3")
+    j, v = m.full_forward(cu(pose), cu(betas), cu(expr), cu(transl))
+    torch.cuda.synchronize()
+    assert torch.isfinite(v).all()
+    for i in sorted({0, min(1023, B - 1), min(1024, B - 1), B - 1}):
+        j1, v1 = m.full_forward(cu(pose[i:i + 1]), cu(betas[i:i + 1]), cu(expr[i:i + 1]), cu(transl[i:i + 1]))
+        assert torch.equal(v[i:i + 1], v1) and torch.equal(j[i:i + 1], j1), i
+    _, vr = sl.smplx_forward(consts, pose[-1:], betas[-1:], expr[-1:], transl[-1:])
+    assert np.abs(v[-1:].cpu().numpy() - vr).max() < TOL
 
 
 def _write_smplx_npz(path, c, components=400):

@@ -3,7 +3,8 @@
     python scripts/online_trace.py [--win 64] [--pushes 60]
 
 Prints, per phase, when its tasks took their tickets, when their inputs were
-ready and when they finished, relative to the step's first ticket (us)."""
+staged (every element carried the launch's tag) and when they finished,
+relative to the step's first ticket (us)."""
 import argparse, ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["TIK_ONLINE_TRACE"] = "1"
@@ -47,18 +48,18 @@ def main():
     phases = []
     for l in range(8):
         phases += [(f"G{l}", nin[l] * couts[l] // 16), (f"T{l}", nout[l] * couts[l] // 16)]
-    phases += [("H0", 512 // 16), ("H1", (66 + 15) // 16)]
+    phases += [("H", 512 // 16)]
     assert sum(c for _, c in phases) == n, (n, phases)
     k = 0
     print(f"{n} tasks, {len(set(tr[:, 7].astype(int)))} workgroups; step span {us[:, 6].max():.1f} us")
-    print(f"{'phase':6s} {'tasks':>5s} {'grab':>14s} {'ready':>14s} {'done':>14s} {'run(ready->done)':>17s}")
+    print(f"{'phase':6s} {'tasks':>5s} {'grab':>14s} {'staged':>14s} {'done':>14s} {'run(staged->done)':>18s}")
     for name, c in phases:
-        g, r, d = us[k:k + c, 0], us[k:k + c, 1], us[k:k + c, 6]
+        g, q, r, d = us[k:k + c, 0], us[k:k + c, 1], us[k:k + c, 2], us[k:k + c, 6]
         extra = ""
         if name[0] in "GT":
-            st, cp, rd, sd = us[k:k + c, 2], us[k:k + c, 3], us[k:k + c, 4], us[k:k + c, 5]
-            extra = (f"  | stage {np.mean(st - r):4.2f} compute {np.mean(cp - st):4.2f} reduce {np.mean(rd - cp):4.2f}"
-                     f" epi+store {np.mean(sd - rd):4.2f} count {np.mean(d - sd):4.2f}")
+            cp, rd, sd = us[k:k + c, 3], us[k:k + c, 4], us[k:k + c, 5]
+            extra = (f"  | wait+load {np.mean(r - q):4.2f} compute {np.mean(cp - r):4.2f} reduce {np.mean(rd - cp):4.2f}"
+                     f" epi+store {np.mean(sd - rd):4.2f} end {np.mean(d - sd):4.2f}")
         print(f"{name:6s} {c:5d} {g.min():6.1f}-{g.max():6.1f} {r.min():6.1f}-{r.max():6.1f} {d.min():6.1f}-{d.max():6.1f}"
               f"   mean {np.mean(d - r):5.2f} max {np.max(d - r):5.2f}{extra}")
         k += c

@@ -700,7 +700,8 @@ int model_online_fill(tik_model* m, tik::OnlineArgs& a) {
         o.cin = L.cin; o.cinp = L.cinp; o.cout = L.cout; o.stride = L.stride; o.res = L.res;
         o.wg = L.wg.p; o.bias2 = L.bias2.p; o.amix = L.amix.p; o.wt = L.wt.p; o.wr = L.wr.p; o.biasT = L.biasT.p;
     }
-    if (m->feat % 4 || m->feat > tik::ONL_MAXHC * 256 || m->hidden % 16 || m->hidden > tik::ONL_MAXHC * 256)
+    if (m->feat % 4 || m->feat > tik::ONL_MAXHC * 256 || m->hidden % 16 || m->hidden > tik::ONL_MAXHC * 256 ||
+        m->pose_dim > 256)   // head tasks: one thread per pose value, W3 columns in LDS
         return fail(TIK_E_INVALID, "online kernel: head %d -> %d", m->feat, m->hidden);
     a.w0 = m->w0.p; a.b0 = m->b0.p; a.w3 = m->w3.p; a.b3 = m->b3.p;
     a.feat = m->feat; a.hidden = m->hidden; a.pose_dim = m->pose_dim;

@@ -12,10 +12,12 @@
 //          clamp, root-relative, data_bn; the pushed frame is read from pinned
 //          host memory and appended to the ring by the launch's last workgroup)
 //   T_L(t, 16 channels): 3x1 temporal conv + residual + bias + ReLU
-//   H0(16 hidden units), H1(16 pose values, written straight to pinned host memory)
-// Workgroups take task tickets in order and wait only on per-frame completion
-// counters of the frames a task reads (no grid-wide barrier), so the layers
-// pipeline frame by frame; a task's weights are loaded before it waits.
+//   H(16 hidden units + their share of the pose; the last H task sums the shares
+//          and writes the pose straight to pinned host memory)
+// Workgroups take task tickets in order and wait only for the activation
+// elements a task reads (tagged with the launch's parity, online.hip; no
+// grid-wide barrier), so the layers pipeline frame by frame; a task's weights
+// are loaded before it waits.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -23,8 +25,8 @@ namespace tik {
 
 constexpr int ONL_MAXL = 12;        // layers
 constexpr int ONL_MAXC = 256;       // channels per layer
-constexpr int ONL_MAXHC = 20;       // head K chunks of 4 per lane: K <= 20 * 4 * 64 = 5120
-enum { ONP_G = 1, ONP_T = 2, ONP_H0 = 3, ONP_H1 = 4 };
+constexpr int ONL_MAXHC = 17;       // head K chunks of 4 per lane: K <= 17 * 4 * 64 = 4352 = 17 joints x ONL_MAXC
+enum { ONP_G = 1, ONP_T = 2, ONP_H = 3 };
 enum { ONR_ZERO = 0, ONR_IDEN = 1, ONR_CONV = 2 };
 
 struct OnlineLayer {
@@ -37,7 +39,7 @@ struct OnlineLayer {
 };
 
 struct OnlinePhase {
-    int kind, layer, nframes, ngroups, task0, cbase;   // cbase: first completion counter (one per frame)
+    int kind, layer, nframes, ngroups, task0, cbase;   // cbase: the phase's counter (the head's: tasks done)
 };
 
 struct OnlineArgs {
@@ -53,7 +55,7 @@ struct OnlineArgs {
     // head
     const float *w0, *b0, *w3, *b3;
     int feat, hidden, pose_dim;
-    float* hid;
+    float* hpart;         // [hidden / 16][pose_dim]: each head task's share of pose_regressor.3
     float* pose;          // device copy of the pose row
     float* pose_host;     // pinned host copy
     int* done_host;       // pinned host word: the frame count after this step, written last (the host spins on it)
@@ -63,8 +65,8 @@ struct OnlineArgs {
     int* cnt;
     int ncnt;
     int* err;             // sticky: a dependency wait timed out
-    unsigned long long* trace;   // debug (TIK_ONLINE_TRACE=1): per task {grab, inputs ready, done, workgroup}
-    float* act;           // the one buffer every inter-task activation lives in (z, out, hid)
+    unsigned long long* trace;   // debug (TIK_ONLINE_TRACE=1): per task 7 time stamps + the workgroup
+    float* act;           // the one buffer every inter-task activation lives in (z, out, hpart, pose)
     unsigned act_bytes;
 };
 

@@ -8,9 +8,10 @@
 // workgroup (16 waves: 4 per SIMD, so LDS and memory latency overlap); the
 // task's weights are loaded into registers BEFORE it waits for its inputs,
 // and the input rows are staged into LDS with coalesced 16-B loads. A task's
-// 17 joints x 16 channels are two 16 x 16 MFMA blocks; its K (input channels,
-// x 3 taps, + the residual conv) is split over 8 wave pairs, and the 8 partial
-// blocks are summed through LDS in a fixed order (deterministic for any grid).
+// 17 joints x 16 channels are one 16 x 16 MFMA block (joints 0-15) + joint 16
+// on the VALU; its K (input channels, x 3 taps, + the residual conv) is split
+// over the 16 waves, and the 16 partial blocks are summed through LDS in a
+// fixed order (deterministic for any grid).
 // (Round 2's VALU version spent 2-3 us per temporal-conv task in its FMAs and
 // the 64-way reduction, profiles/r02_v2_online_trace.txt.)
 //
@@ -18,11 +19,13 @@
 // task hands to another task is stored and loaded with device-scope cache
 // policy (sc1: written through to / read from the device coherence point), the
 // encoding the compiler uses for agent-scope atomic loads and stores; the
-// weights stay ordinary cached loads (read-only for the whole launch). A
-// producer waits for its stores (vmcnt(0) in every wave) and then bumps the
-// frame's completion counter (device-scope atomic); a consumer polls the
-// counter and only then issues its loads. No L2 write-back or invalidate: a
-// first version with agent-scope release/acquire fences (buffer_wbl2 /
+// weights stay ordinary cached loads (read-only for the whole launch). The
+// activations are ReLU outputs, so their sign bit carries the launch's parity
+// and a consumer polls the elements it reads until all carry it: no producer
+// waits for its stores, no completion counters (round 5: a per-frame counter
+// cost a store acknowledgement + counter update + counter poll + data load per
+// dependency, ~1.5 us of the ~3.5 us per hop). No L2 write-back or invalidate:
+// a first version with agent-scope release/acquire fences (buffer_wbl2 /
 // buffer_inv per task) spent most of its time in them (213 us per step).
 // Tickets are taken in topological order, so the smallest unfinished taken
 // task always has its inputs complete: no deadlock, whatever the residency.
@@ -36,6 +39,8 @@ namespace onl {
 constexpr int NT = 1024;
 constexpr int LDP = 4;                                    // row padding (floats): MFMA A reads conflict-free
 constexpr int SMF = 4 * 17 * (ONL_MAXC + LDP);            // staged rows, floats (70,720 B)
+constexpr int RED = 16 * 272;                              // the 16 waves' partial 17 x 16 blocks (after SMF)
+constexpr int SMT = SMF + RED + 272;                       // + y[17][16]
 constexpr unsigned long long TIMEOUT = 50000000ull;      // s_memrealtime ticks (100 MHz)
 }  // namespace onl
 
@@ -52,43 +57,47 @@ __device__ __forceinline__ Act act_of(const OnlineArgs* __restrict__ A) {
     return Act{__builtin_amdgcn_make_buffer_rsrc(A->act, 0, (int)A->act_bytes, 0x00020000), reinterpret_cast<const char*>(A->act)};
 }
 __device__ __forceinline__ int act_off(const Act& b, const float* p) { return (int)(reinterpret_cast<const char*>(p) - b.base); }
-__device__ __forceinline__ float4 ld4c(const Act& b, const float* p) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(b.r, act_off(b, p), 0, CPOL_SC1));
-}
-__device__ __forceinline__ void st4c(const Act& b, float* p, const float4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), b.r, act_off(b, p), 0, CPOL_SC1);
-}
 __device__ __forceinline__ void st1c(const Act& b, float* p, const float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), b.r, act_off(b, p), 0, CPOL_SC1);
 }
+__device__ void onl_mark(const OnlineArgs* __restrict__ A, int task, int k);
 
-// thread 0 only: wait until *cnt[ci] >= target
-__device__ void onl_wait(const OnlineArgs* __restrict__ A, int ci, int target) {
-    int* p = A->cnt + ci;
-    if (cnt_load(p) >= target) return;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (cnt_load(p) < target) {
-        if (cnt_load(A->err)) return;
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > onl::TIMEOUT) {
-            __hip_atomic_fetch_or(A->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
+// ---- tagged activations. Every G / T output is a ReLU value (>= +0), so its sign
+// bit is free: launch c stores v | (c & 1) << 31, and a consumer polls the data itself
+// until each element carries this launch's tag. A dependency costs one trip through
+// memory (no store acknowledgement before a completion count, no count poll, no
+// data load after it). Every launch runs the same task list and so rewrites every
+// element it reads; the buffer starts at tag 1 (setup, reset) for launch 0.
+__device__ __forceinline__ u32x4 ld4raw(const Act& b, const float* p) {
+    return __builtin_amdgcn_raw_buffer_load_b128(b.r, act_off(b, p), 0, CPOL_SC1);
+}
+__device__ __forceinline__ bool tag_ok(const u32x4 r, const unsigned E) {
+    return ((((r.x ^ E) | (r.y ^ E)) | ((r.z ^ E) | (r.w ^ E))) >> 31) == 0;
+}
+// r: the first load of p; polls until tagged E (or the error flag / a timeout), untags
+__device__ __forceinline__ float4 onl_fin4(const OnlineArgs* __restrict__ A, const Act& b, const float* p, const unsigned E, u32x4 r) {
+    if (!tag_ok(r, E)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (int it = 1;; ++it) {
+            asm volatile("" ::: "memory");
+            r = ld4raw(b, p);
+            if (tag_ok(r, E)) break;
+            if ((it & 63) == 0 && (cnt_load(A->err) || __builtin_amdgcn_s_memrealtime() - t0 > onl::TIMEOUT)) {
+                __hip_atomic_fetch_or(A->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
         }
     }
+    const unsigned m = 0x7fffffffu;
+    return make_float4(__builtin_bit_cast(float, r.x & m), __builtin_bit_cast(float, r.y & m), __builtin_bit_cast(float, r.z & m),
+                       __builtin_bit_cast(float, r.w & m));
+}
+__device__ __forceinline__ void st1t(const Act& b, float* p, const float v, const unsigned E) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v) | E, b.r, act_off(b, p), 0, CPOL_SC1);
 }
 
-// all threads: this task's stores are complete and visible device-wide, then count it
-__device__ void onl_mark(const OnlineArgs* __restrict__ A, int task, int k);
-__device__ void onl_release(const OnlineArgs* __restrict__ A, int ci, int task) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        onl_mark(A, task, 5);
-        __hip_atomic_fetch_add(A->cnt + ci, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// debug trace: slot k of task `task` (thread 0 only)
+// debug trace: slot k of task `task` (thread 0 only): 0 ticket, 1 inputs requested,
+// 2 inputs staged, 3 products, 4 reduced, 5 stored, 6 task end
 __device__ void onl_mark(const OnlineArgs* __restrict__ A, int task, int k) {
     if (A->trace) A->trace[8 * (size_t)task + k] = __builtin_amdgcn_s_memrealtime();
 }
@@ -140,13 +149,15 @@ typedef float onl_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int ONL_KSL = 16;   // K slices (one per wave)
 
 // the 16 waves' partials (acc: joints 0-15; p16: joint 16 of lane l's channel and K
-// element) -> y[v][co] at sm[16 * 272 + 16 v + co] (threads 0-271 read it), summed in a fixed order
-__device__ __forceinline__ void onl_reduce_mfma(const onl_f32x4 acc, float p16, float* sm) {
+// element) -> y[v][co] at sm[SMF + RED + 16 v + co], summed in a fixed order; the
+// partials have their own LDS (no barrier for the staged rows' last reads). With
+// sync_y the y block is visible to every thread on return (the gcn mix reads all
+// 17 joints); without, thread tid < 272 reads only its own y[tid].
+__device__ __forceinline__ void onl_reduce_mfma(const onl_f32x4 acc, float p16, float* sm, bool sync_y) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     p16 += __shfl_xor(p16, 16);
     p16 += __shfl_xor(p16, 32);
-    __syncthreads();   // every staged-row read done: the LDS is reused
-    float* red = sm;   // [16 waves][17 joints][16 co]
+    float* red = sm + onl::SMF;   // [16 waves][17 joints][16 co]
 #pragma unroll
     for (int e = 0; e < 4; ++e) red[wave * 272 + (4 * (lane >> 4) + e) * 16 + (lane & 15)] = acc[e];
     if (lane < 16) red[wave * 272 + 16 * 16 + lane] = p16;
@@ -155,13 +166,13 @@ __device__ __forceinline__ void onl_reduce_mfma(const onl_f32x4 acc, float p16, 
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < ONL_KSL; ++k) s += red[k * 272 + tid];
-        sm[16 * 272 + tid] = s;
+        sm[onl::SMF + onl::RED + tid] = s;
     }
-    __syncthreads();
+    if (sync_y) __syncthreads();
 }
 
 // ---- G_L(f, 16 channels): z = ReLU(bias2 + sum_v A[v][w] (x . wg^T)[v])
-__device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task) {
+__device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task, const unsigned E) {
     const OnlinePhase& ph = A->ph[p];
     const OnlineLayer& L = A->L[ph.layer];
     int tid = threadIdx.x;
@@ -190,23 +201,27 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
     onl_hold(b);
 #pragma unroll
     for (int v = 0; v < 17; ++v) onl_hold(am[v]);
-    if (tid == 0) {
-        if (ph.layer > 0) {   // the previous temporal conv's frame f
-            const OnlinePhase& pp = A->ph[p - 1];
-            onl_wait(A, pp.cbase + f, pp.ngroups);
-        }
-        onl_mark(A, task, 1);
-    }
-    __syncthreads();
     float4* s4 = reinterpret_cast<float4*>(sm);
     const Act ab = act_of(A);
+    if (tid == 0) onl_mark(A, task, 1);
     if (ph.layer == 0) {
         onl_raw_rows(A, f, s4, LD / 4);
-    } else {
+    } else {   // the previous temporal conv's frame f, all 17 x cinp loads in flight at once
+        constexpr int NL = (17 * ONL_MAXC / 4 + onl::NT - 1) / onl::NT;
         const float* xr = L.x + (size_t)f * 17 * cinp;
-        for (int i = tid; i < 17 * K4; i += onl::NT) {
-            const int v = i / K4;
-            s4[v * (LD / 4) + (i - v * K4)] = ld4c(ab, xr + 4 * i);
+        u32x4 r[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (i < 17 * K4) r[j] = ld4raw(ab, xr + 4 * i);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (i < 17 * K4) {
+                const int v = i / K4;
+                s4[v * (LD / 4) + (i - v * K4)] = onl_fin4(A, ab, xr + 4 * i, E, r[j]);
+            }
         }
     }
     __syncthreads();
@@ -224,25 +239,24 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
         }
     }
     if (tid == 0) onl_mark(A, task, 3);
-    onl_reduce_mfma(acc[0] + acc[1], p16, sm);
+    onl_reduce_mfma(acc[0] + acc[1], p16, sm, true);
     if (tid == 0) onl_mark(A, task, 4);
-    const float* y = sm + 16 * 272;
+    const float* y = sm + onl::SMF + onl::RED;
     if (tid < 272) {
         float s = b;
 #pragma unroll
         for (int v = 0; v < 17; ++v) s = fmaf(am[v], y[v * 16 + co], s);
-        st1c(ab, L.z + (size_t)(f * 17 + wo) * cout + c0 + co, s > 0.f ? s : 0.f);
+        st1t(ab, L.z + (size_t)(f * 17 + wo) * cout + c0 + co, s > 0.f ? s : 0.f, E);
     }
-    onl_release(A, ph.cbase + f, task);
+    if (tid == 0) onl_mark(A, task, 5);
 }
 
 // ---- T_L(t, 16 channels): out = ReLU(sum_tap z[s t + tap - 1] . wt_tap^T + bias + residual)
 // Staged operand rows, one per joint, in K order: [z tap 0 (C) | tap 1 | tap 2 | block
 // input x (cinp: the residual conv's K segment, or the identity term)], so K step sk
 // reads floats 4 sk .. of the row (no per-step tap decode between the MFMAs)
-__device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task) {
+__device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task, const unsigned E) {
     const OnlinePhase& ph = A->ph[p];
-    const OnlinePhase& pg = A->ph[p - 1];   // this layer's gcn
     const OnlineLayer& L = A->L[ph.layer];
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));   // lane-derived offsets are made per task, not hoisted across the task loop (spills)
@@ -267,32 +281,55 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     const float bt = L.biasT[c0 + (tid & 15)];
 #pragma unroll
     for (int q = 0; q < NS; ++q) onl_hold(w[q]);
-    if (tid == 0) {
-#pragma unroll
-        for (int tap = 0; tap < 3; ++tap) {
-            const int fr = fx + tap - 1;
-            if (fr >= 0 && fr < tin) onl_wait(A, pg.cbase + fr, pg.ngroups);
-        }
-        onl_mark(A, task, 1);
-    }
-    __syncthreads();
+    // staging: the block input rows (the previous layer's temporal conv, frame fx) and
+    // the three z frames, every load in flight at once; each element is then polled
+    // until it carries this launch's tag (usually only the newest frame's)
     float4* s4 = reinterpret_cast<float4*>(sm);
     const int nz = 17 * C4;
     const Act ab = act_of(A);
-    for (int i = tid; i < 3 * nz; i += onl::NT) {
-        const int tap = i >= 2 * nz ? 2 : (i >= nz ? 1 : 0);
-        const int fr = fx + tap - 1, r = i - tap * nz, v = r / C4;
-        s4[v * LK4 + tap * C4 + (r - v * C4)] =
-            (fr >= 0 && fr < tin) ? ld4c(ab, L.z + ((size_t)fr * nz + r) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int NL = (17 * ONL_MAXC / 4 + onl::NT - 1) / onl::NT;   // loads per thread per row block
+    const bool xin = L.res != ONR_ZERO && ph.layer > 0;
+    const float* xrow = xin ? L.x + (size_t)fx * 17 * L.cinp : L.z;
+    if (tid == 0) onl_mark(A, task, 1);
+    u32x4 rx[NL], rz[3][NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        const int i = tid + j * onl::NT;
+        if (xin && i < 17 * cinp4) rx[j] = ld4raw(ab, xrow + 4 * i);
     }
-    const float* xrow = L.x + (size_t)fx * 17 * L.cinp;
-    if (ph.layer == 0 && L.res != ONR_ZERO)
-        onl_raw_rows(A, fx, s4 + 3 * C4, LK4);
-    else if (L.res != ONR_ZERO)   // residual rows: the conv's K segment, or the identity term
-        for (int i = tid; i < 17 * cinp4; i += onl::NT) {
-            const int v = i / cinp4;
-            s4[v * LK4 + 3 * C4 + (i - v * cinp4)] = ld4c(ab, xrow + 4 * i);
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+        const int fr = fx + tap - 1;
+        const bool live = fr >= 0 && fr < tin;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (live && i < nz) rz[tap][j] = ld4raw(ab, L.z + ((size_t)fr * nz + i) * 4);
         }
+    }
+    if (L.res != ONR_ZERO && ph.layer == 0) onl_raw_rows(A, fx, s4 + 3 * C4, LK4);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        const int i = tid + j * onl::NT;
+        if (xin && i < 17 * cinp4) {
+            const int v = i / cinp4;
+            s4[v * LK4 + 3 * C4 + (i - v * cinp4)] = onl_fin4(A, ab, xrow + 4 * i, E, rx[j]);
+        }
+    }
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+        const int fr = fx + tap - 1;
+        const bool live = fr >= 0 && fr < tin;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (i < nz) {
+                const int v = i / C4;
+                s4[v * LK4 + tap * C4 + (i - v * C4)] =
+                    live ? onl_fin4(A, ab, L.z + ((size_t)fr * nz + i) * 4, E, rz[tap][j]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    }
     __syncthreads();
     if (tid == 0) onl_mark(A, task, 2);
     // identity residual of this thread's output (v = tid / 16, threads 0-271),
@@ -313,46 +350,63 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     }
     const onl_f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     if (tid == 0) onl_mark(A, task, 3);
-    onl_reduce_mfma(accs, p16, sm);
+    onl_reduce_mfma(accs, p16, sm, false);
     if (tid == 0) onl_mark(A, task, 4);
     if (tid < 272) {
-        const float r = sm[16 * 272 + tid] + bt + res;
-        st1c(ab, L.out + (size_t)(t * 17 + (tid >> 4)) * C + c0 + (tid & 15), r > 0.f ? r : 0.f);
+        const float r = sm[onl::SMF + onl::RED + tid] + bt + res;
+        st1t(ab, L.out + (size_t)(t * 17 + (tid >> 4)) * C + c0 + (tid & 15), r > 0.f ? r : 0.f, E);
     }
-    onl_release(A, ph.cbase + t, task);
+    if (tid == 0) onl_mark(A, task, 5);
 }
 
-// ---- H0 (16 hidden units, one per wave) and H1 (16 pose values, one per wave)
-template <bool FIRST>
-__device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task) {
+// ---- the head: task idx = hidden units 16 idx .. 16 idx + 15 (one per wave) of
+// pose_regressor.0 + LeakyReLU, and right away their share of pose_regressor.3:
+// part[idx][o] = sum_u W3[o][16 idx + u] h[16 idx + u] (threads o < pose_dim, the 16
+// W3 columns prefetched). The last head task to finish (its counter add returns
+// ngroups - 1) sums the parts in task order, + b3, and writes the pose: no
+// separate second-layer task and dependency hop.
+__device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task, const unsigned E) {
     const OnlinePhase& ph = A->ph[p];
-    const OnlinePhase& pp = A->ph[p - 1];
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int u = tid >> 6, lane = tid & 63;
-    const int j = 16 * idx + u;                         // output index
-    const int nout = FIRST ? A->hidden : A->pose_dim;
-    const int K4 = (FIRST ? A->feat : A->hidden) >> 2;
-    const float4* w4 = reinterpret_cast<const float4*>((FIRST ? A->w0 : A->w3) + (size_t)(j < nout ? j : 0) * 4 * K4);
+    const int j = 16 * idx + u;                         // hidden unit of this wave
+    const int nout = A->hidden, npose = A->pose_dim;
+    const int K4 = A->feat >> 2;
+    const float4* w4 = reinterpret_cast<const float4*>(A->w0 + (size_t)(j < nout ? j : 0) * 4 * K4);
     float4 w[ONL_MAXHC];
 #pragma unroll
     for (int i = 0; i < ONL_MAXHC; ++i) {
         const int k = lane + 64 * i;
         w[i] = (k < K4 && j < nout) ? w4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float b = j < nout ? (FIRST ? A->b0 : A->b3)[j] : 0.f;
+    const float b = j < nout ? A->b0[j] : 0.f;
+    // this task's 16 columns of W3, staged in LDS (the reduction area) before the wait
+    float* hs = sm + onl::SMF;          // [16] hidden values, then [npose][16] W3 columns
+    float* hw3 = hs + 16;
+    for (int i = tid; i < 16 * npose; i += onl::NT) hw3[i] = A->w3[(size_t)(i >> 4) * nout + 16 * idx + (i & 15)];
 #pragma unroll
     for (int i = 0; i < ONL_MAXHC; ++i) onl_hold(w[i]);
-    if (tid == 0) {
-        onl_wait(A, pp.cbase, pp.ngroups);   // T_last frame 0 / all of H0
-        onl_mark(A, task, 1);
-    }
-    __syncthreads();
+    if (tid == 0) onl_mark(A, task, 1);
     float4* s4 = reinterpret_cast<float4*>(sm);
     const Act ab = act_of(A);
-    const float* in = FIRST ? A->L[A->nl - 1].out : A->hid;
-    for (int i = tid; i < K4; i += onl::NT) s4[i] = ld4c(ab, in + 4 * i);   // the (17*C) feature of frame 0 / the hidden vector
+    const float* in = A->L[A->nl - 1].out;   // the (17*C) feature of frame 0
+    {
+        constexpr int NL = (ONL_MAXHC * 64 + onl::NT - 1) / onl::NT;
+        u32x4 r[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (i < K4) r[j] = ld4raw(ab, in + 4 * i);
+        }
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const int i = tid + j * onl::NT;
+            if (i < K4) s4[i] = onl_fin4(A, ab, in + 4 * i, E, r[j]);
+        }
+    }
     __syncthreads();
+    if (tid == 0) onl_mark(A, task, 2);
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < ONL_MAXHC; ++i) {
@@ -361,33 +415,59 @@ __device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (!FIRST && idx == 0 && tid == 0)
-        __hip_atomic_store(A->pose_host + A->pose_dim, cnt_load(A->err) ? 1.f : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (lane == 0 && j < nout) {
-        float r = acc + b;
-        if (FIRST) {
-            st1c(ab, A->hid + j, r > 0.f ? r : 0.01f * r);
-        } else {
-            A->pose[j] = r;
-            __hip_atomic_store(A->pose_host + j, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __shared__ int s_lastp;
+    if (lane == 0) {
+        const float r = acc + b;
+        hs[u] = j < nout ? (r > 0.f ? r : 0.01f * r) : 0.f;
+    }
+    __syncthreads();
+    if (tid < npose) {
+        float q = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) q = fmaf(hw3[16 * tid + e], hs[e], q);
+        st1c(ab, A->hpart + (size_t)idx * npose + tid, q);
+    }
+    // stores complete in every wave, then count this task; the last one finishes the pose
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        onl_mark(A, task, 5);
+        s_lastp = __hip_atomic_fetch_add(A->cnt + ph.cbase, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ph.ngroups - 1;
+    }
+    __syncthreads();
+    if (!s_lastp) return;
+    if (tid < npose) {
+        float r = A->b3[tid];
+        for (int k0 = 0; k0 < ph.ngroups; k0 += 16) {   // 16 loads in flight, summed in task order
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                v[k] = k0 + k < ph.ngroups ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 ab.r, act_off(ab, A->hpart + (size_t)(k0 + k) * npose + tid), 0, CPOL_SC1))
+                                           : 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k0 + k < ph.ngroups) r += v[k];
         }
+        A->pose[tid] = r;
+        __hip_atomic_store(A->pose_host + tid, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (FIRST) {
-        onl_release(A, ph.cbase, task);
-    } else {
-        // the pose stores (system scope, to pinned host memory) complete before this
-        // workgroup's done count, which the last workgroup waits for before it
-        // signals the host (no L2 write-back fence: ~23 us measured)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if (tid == 0)
+        __hip_atomic_store(A->pose_host + npose, cnt_load(A->err) ? 1.f : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the pose stores (system scope, to pinned host memory) complete before this
+    // workgroup's done count, which the last workgroup waits for before it signals
+    // the host (no L2 write-back fence: ~23 us measured)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restrict__ A) {
-    __shared__ float4 sm4[onl::SMF / 4];
+    __shared__ float4 sm4[onl::SMT / 4];
     __shared__ int s_task, s_last;
     float* sm = reinterpret_cast<float*>(sm4);
     const int tid = threadIdx.x;
+    // this launch's activation tag (count: frames pushed before it, bumped by the previous launch's last workgroup)
+    const unsigned E = (unsigned)(cnt_load(A->count) & 1) << 31;
     for (;;) {
         if (tid == 0) s_task = __hip_atomic_fetch_add(A->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -398,10 +478,9 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
         while (p + 1 < A->nph && task >= A->ph[p + 1].task0) ++p;
         const int idx = task - A->ph[p].task0;
         switch (A->ph[p].kind) {
-            case ONP_G: onl_gcn(A, p, idx, sm, task); break;
-            case ONP_T: onl_tconv(A, p, idx, sm, task); break;
-            case ONP_H0: onl_head<true>(A, p, idx, sm, task); break;
-            default: onl_head<false>(A, p, idx, sm, task); break;
+            case ONP_G: onl_gcn(A, p, idx, sm, task, E); break;
+            case ONP_T: onl_tconv(A, p, idx, sm, task, E); break;
+            default: onl_head(A, p, idx, sm, task, E); break;
         }
         if (tid == 0 && A->trace) {
             onl_mark(A, task, 6);
@@ -421,8 +500,8 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
             A->count[0] = c + 1;
             A->ticket[0] = 0;
             A->done[0] = 0;
-            // the H1 task (done: every task has run) already published the flag to
-            // pose_host; a timeout must not leak into the next launch's waits
+            // the last head task (done: every task has run) already published the flag
+            // to pose_host; a timeout must not leak into the next launch's waits
             A->err[0] = 0;
             // every read of the pushed frame and every pose store is done: tell the
             // host (it spins on this word instead of waiting for the kernel's end)

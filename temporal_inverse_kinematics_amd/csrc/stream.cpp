@@ -82,7 +82,7 @@ static int setup_online(tik_stream* s) {
         L.n_in = std::min(L.tin, L.stride * (need - 1) + 2);
         need = L.n_in;
     }
-    size_t tot = (size_t)a.hidden + ((a.pose_dim + 3) & ~3);
+    size_t tot = (size_t)(a.hidden / 16) * a.pose_dim + ((a.pose_dim + 3) & ~3);
     for (int l = 0; l < nl; ++l) tot += (size_t)(a.L[l].n_in + a.L[l].n_out) * 17 * a.L[l].cout;
     if ((rc = s->onl_act.reserve(tot))) return rc;
     float* q = s->onl_act.p;
@@ -92,22 +92,23 @@ static int setup_online(tik_stream* s) {
         L.z = q; q += (size_t)L.n_in * 17 * L.cout;
         L.out = q; q += (size_t)L.n_out * 17 * L.cout;
     }
-    a.hid = q; q += a.hidden;
+    a.hpart = q; q += (size_t)(a.hidden / 16) * a.pose_dim;
     a.pose = q;
     a.act = s->onl_act.p;
     a.act_bytes = (unsigned)(tot * sizeof(float));
+    // every G / T output carries its launch's tag (online.hip): start at tag 1, for launch 0
+    HIP_TRY(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s->onl_act.p), (int)0x80000000u, s->onl_act.n));
     int np = 0, task = 0, cb = 0;
     auto add = [&](int kind, int layer, int nf, int ng) {
         a.ph[np++] = tik::OnlinePhase{kind, layer, nf, ng, task, cb};
         task += nf * ng;
-        cb += nf;
+        if (kind == tik::ONP_H) ++cb;   // the head's one counter (G / T hand over tagged data)
     };
     for (int l = 0; l < nl; ++l) {
         add(tik::ONP_G, l, a.L[l].n_in, a.L[l].cout / 16);
         add(tik::ONP_T, l, a.L[l].n_out, a.L[l].cout / 16);
     }
-    add(tik::ONP_H0, nl - 1, 1, a.hidden / 16);
-    add(tik::ONP_H1, nl - 1, 1, (a.pose_dim + 15) / 16);
+    add(tik::ONP_H, nl - 1, 1, a.hidden / 16);
     a.nph = np;
     a.ntasks = task;
     if ((rc = s->onl_cnt.reserve(cb + 3))) return rc;
@@ -225,7 +226,11 @@ int tik_stream_reset(tik_stream_t s) {
     if (!s) return fail(TIK_E_INVALID, "null stream");
     HIP_TRY(hipMemsetAsync(s->count.p, 0, sizeof(int), s->st));
     // the dataflow kernel's scheduling state: completion counters, ticket, done, err
-    if (s->online) HIP_TRY(hipMemsetAsync(s->onl_cnt.p, 0, sizeof(int) * s->onl_cnt.n, s->st));
+    if (s->online) {
+        HIP_TRY(hipMemsetAsync(s->onl_cnt.p, 0, sizeof(int) * s->onl_cnt.n, s->st));
+        // count restarts at 0: the activations go back to tag 1 (online.hip)
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s->onl_act.p), (int)0x80000000u, s->onl_act.n, s->st));
+    }
     HIP_TRY(hipStreamSynchronize(s->st));
     s->host_pose[s->pose_dim] = 0.f;
     *s->host_done = 0;

@@ -27,7 +27,7 @@ def _asm(src_name, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src_name", ["xgemm.hip", "xblock.hip", "xgraph.hip", "xtws.hip", "fk.hip"])
+@pytest.mark.parametrize("src_name", ["xgemm.hip", "xblock.hip", "xgraph.hip", "xtws.hip", "fk.hip", "online.hip"])
 def test_counted_wait_kernels_do_not_spill(tmp_path, src_name):
     """Kernels with counted vmcnt waits (LDS-DMA rings, prefetch across tiles)
     must not spill: a scratch load or store is a vector-memory instruction and

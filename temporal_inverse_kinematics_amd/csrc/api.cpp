@@ -196,7 +196,6 @@ struct Layer {
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers; 0 = the XG tiles)
     int xtwson = 1;         // temporal conv on xtws.hip where packed (TIK_XTWS bit mask of layers; 0 = XT128)
-    int ncu = 256;          // compute units (persistent grid size)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
 
@@ -352,7 +351,7 @@ struct Layer {
     // z: workspace; out: [N*tout*V][cout]. Layer 0 from the raw keypoints
     // (cin <= 4): xraw = (N,T,V,C0) keypoints, its data_bn'd copy goes to xb4
     // ([rows][4]) for the residual conv in the temporal conv's epilogue.
-    int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st,
+    int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st, int ncu,
                   const float* xraw = nullptr, const float* bn_sc = nullptr, const float* bn_sh = nullptr,
                   float* xb4 = nullptr) const {
         const int to = tout(tin, stride);
@@ -490,7 +489,6 @@ static void apply_env(tik_model* md) {
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
         md->ncu = ncu;
     for (auto& L : md->layers) {
-        L.ncu = md->ncu;
         if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
         if (const char* w = getenv("TIK_XTWS")) L.xtwson = (atoi(w) >> L.index) & 1;
         L.xtrash = reinterpret_cast<float*>(md->trash.p);
@@ -719,8 +717,9 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
 
 struct WsPtrs {
     float *xb, *z, *a0, *a1, *hid, *part;
+    int ncu;   // persistent grids: the CUs this part runs on
 };
-static WsPtrs ptrs_of(const Workspace& w) { return WsPtrs{w.xb.p, w.z.p, w.a0.p, w.a1.p, w.hid.p, w.part.p}; }
+static WsPtrs ptrs_of(const Workspace& w, int ncu) { return WsPtrs{w.xb.p, w.z.p, w.a0.p, w.a1.p, w.hid.p, w.part.p, ncu}; }
 // the workspaces and aux streams of the parts 1 .. np-1 of a split batch
 static int reserve_parts(tik_model* m, int np, int N, int T) {
     int rc;
@@ -836,7 +835,7 @@ static int blocks01_x(tik_model_t m, const float* x, int N, int T, float* out, h
     {
         ProfScope p("XB0.L0", 2.0 * px * (L0.cin * 64 + 17 * 64) + 2.0 * px * (TK * 64 * 64 + L0.cin * 64), px * (4.0 * m->C0 + 384.0), st);
         p.out(p3, (size_t)px * 384);
-        HIP_TRY(launch_xblock_traced(b, true, m->ncu, st, "XB0.L0"));
+        HIP_TRY(launch_xblock_traced(b, true, w.ncu, st, "XB0.L0"));
     }
     tik::XBlkArgs c{};
     c.nframes = N * T; c.T = T; c.xp3 = p3;
@@ -845,7 +844,7 @@ static int blocks01_x(tik_model_t m, const float* x, int N, int T, float* out, h
     {
         ProfScope p("XB1.L1", 2.0 * px * (64 * 64 + 17 * 64) + 2.0 * px * TK * 64 * 64, px * (384.0 + 256.0), st);
         p.out(out, (size_t)px * 256);
-        HIP_TRY(launch_xblock_traced(c, false, m->ncu, st, "XB1.L1"));
+        HIP_TRY(launch_xblock_traced(c, false, w.ncu, st, "XB1.L1"));
     }
     return TIK_OK;
 }
@@ -864,8 +863,8 @@ static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_
     for (const Layer& L : m->layers) {
         if (xblk && L.index < 2) continue;
         float* o = bufs[which];
-        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, x, m->bn_sc.p, m->bn_sh.p, w.xb);
-        else rc = L.forward_x(cur, ld, N, t, w.z, o, st);
+        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, w.ncu, x, m->bn_sc.p, m->bn_sh.p, w.xb);
+        else rc = L.forward_x(cur, ld, N, t, w.z, o, st, w.ncu);
         if (rc) return rc;
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
@@ -885,7 +884,7 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
         for (int n0 = 0; n0 < N; n0 += chunk) {
             const int n = std::min(chunk, N - n0);
             float* f;
-            if ((rc = backbone_x(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &to, st, ptrs_of(m->ws[0])))) return rc;
+            if ((rc = backbone_x(m, x + (size_t)n0 * T * m->V * m->C0, n, T, &f, &to, st, ptrs_of(m->ws[0], m->ncu)))) return rc;
             HIP_TRY(hipMemcpyAsync(feat + (size_t)n0 * to * m->feat, f, sizeof(float) * (size_t)n * to * m->feat,
                                    hipMemcpyDeviceToDevice, st));
         }
@@ -893,7 +892,7 @@ int tik_backbone_forward(tik_model_t m, const float* x, int N, int T, float* fea
     }
     if ((rc = tik_model_reserve(m, N, T))) return rc;
     float* f;
-    if ((rc = backbone(m, x, N, T, &f, &to, st, ptrs_of(m->ws[0])))) return rc;
+    if ((rc = backbone(m, x, N, T, &f, &to, st, ptrs_of(m->ws[0], m->ncu)))) return rc;
     HIP_TRY(hipMemcpyAsync(feat, f, sizeof(float) * (size_t)N * to * m->feat, hipMemcpyDeviceToDevice, st));
     return TIK_OK;
 }
@@ -1005,21 +1004,21 @@ int model_forward_ws(tik_model* m, const float* x, int N, int T, float* poses, h
                 for (int k = 0; k < np; ++k) {
                     const int a0 = (int)((long long)n * k / np), a1 = (int)((long long)n * (k + 1) / np);
                     if ((rc = part(xs + (size_t)a0 * T * m->V * m->C0, a1 - a0, ps + (size_t)a0 * To * m->pose_dim,
-                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k]))))
+                                   k == 0 ? st : m->aux[k - 1], ptrs_of(k == 0 ? ws : m->ws[k], m->ncu))))
                         return rc;
                 }
                 for (int k = 1; k < np; ++k) {
                     HIP_TRY(hipEventRecord(m->ev_join[k - 1], m->aux[k - 1]));
                     HIP_TRY(hipStreamWaitEvent(st, m->ev_join[k - 1], 0));
                 }
-            } else if ((rc = part(xs, n, ps, st, ptrs_of(ws)))) {
+            } else if ((rc = part(xs, n, ps, st, ptrs_of(ws, m->ncu)))) {
                 return rc;
             }
         }
         return TIK_OK;
     }
     if ((rc = model_reserve_ws(m, ws, N, T))) return rc;
-    const WsPtrs w = ptrs_of(ws);
+    const WsPtrs w = ptrs_of(ws, m->ncu);
     if ((rc = backbone(m, x, N, T, &f, &to, st, w))) return rc;
     return head_splitk(m, f, N * to, poses, w.hid, w.part, st);
 }

@@ -131,8 +131,10 @@ static int setup_online(tik_stream* s) {
     }
     s->onl_ntasks = task;
     if ((rc = s->onl_args.upload(std::vector<tik::OnlineArgs>{a}))) return rc;
-    // half the CUs: more workgroups only add pollers (measured p50 143 us at 128, 151 us at 256)
-    int grid = std::max(1, cu_count() / 2);
+    // one workgroup per CU (89 KB of LDS each). With per-frame counters half the CUs was best
+    // (143 us at 128 vs 151 us at 256); with tagged data the wider grid wins: p50 81 us at 128,
+    // 74 at 160, 70 at 192, 67 at 256 (profiles/r05_og_ab_online_grid.txt)
+    int grid = std::max(1, cu_count());
     if (const char* e = getenv("TIK_ONLINE_GRID")) grid = std::max(1, std::min(cu_count(), atoi(e)));   // test hook
     s->onl_grid = grid;
     s->online = true;

@@ -436,17 +436,18 @@ __device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float
     }
     __syncthreads();
     if (!s_lastp) return;
+    const int c = cnt_load(A->count);
     if (tid < npose) {
         float r = A->b3[tid];
-        for (int k0 = 0; k0 < ph.ngroups; k0 += 16) {   // 16 loads in flight, summed in task order
-            float v[16];
+        for (int k0 = 0; k0 < ph.ngroups; k0 += 32) {   // 32 loads in flight, summed in task order
+            float v[32];
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
+            for (int k = 0; k < 32; ++k)
                 v[k] = k0 + k < ph.ngroups ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                  ab.r, act_off(ab, A->hpart + (size_t)(k0 + k) * npose + tid), 0, CPOL_SC1))
                                            : 0.f;
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
+            for (int k = 0; k < 32; ++k)
                 if (k0 + k < ph.ngroups) r += v[k];
         }
         A->pose[tid] = r;
@@ -454,11 +455,13 @@ __device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float
     }
     if (tid == 0)
         __hip_atomic_store(A->pose_host + npose, cnt_load(A->err) ? 1.f : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // the pose stores (system scope, to pinned host memory) complete before this
-    // workgroup's done count, which the last workgroup waits for before it signals
-    // the host (no L2 write-back fence: ~23 us measured)
+    // the pose and flag stores (system scope, to pinned host memory) complete in
+    // every wave before the host is told (no L2 write-back fence: ~23 us
+    // measured); the rest of the launch's bookkeeping (counters, count, ticket) is
+    // on the device and ordered before the next launch by the stream
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (tid == 0) __hip_atomic_store(A->done_host, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restrict__ A) {
@@ -477,6 +480,17 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
         int p = 0;
         while (p + 1 < A->nph && task >= A->ph[p + 1].task0) ++p;
         const int idx = task - A->ph[p].task0;
+        if (task == 0) {
+            // the pushed frame into the ring. Slot count % W holds frame count - W,
+            // which no task of this launch reads (frames count - 2h .. count - 1 come
+            // from the ring, frame count from pinned host memory). Task 0 is in every
+            // head task's dependency cone and waits for the load before its own
+            // output stores, so the frame has been read before the host is signalled
+            // and may overwrite its frame buffer.
+            const int c = cnt_load(A->count);
+            if (tid < 17 * 3) A->ring[(size_t)(c % A->W) * 17 * 3 + tid] = A->frame[tid];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         switch (A->ph[p].kind) {
             case ONP_G: onl_gcn(A, p, idx, sm, task, E); break;
             case ONP_T: onl_tconv(A, p, idx, sm, task, E); break;
@@ -493,19 +507,15 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
     __syncthreads();
     if (s_last) {
         for (int i = tid; i < A->ncnt; i += onl::NT) A->cnt[i] = 0;
-        // every task has read the ring and the count: append the pushed frame
-        const int c = cnt_load(A->count);
-        for (int i = tid; i < 17 * 3; i += onl::NT) A->ring[(size_t)(c % A->W) * 17 * 3 + i] = A->frame[i];
         if (tid == 0) {
-            A->count[0] = c + 1;
+            // every task has read the count (the ring append and the host signal are
+            // the last head task's)
+            A->count[0] = cnt_load(A->count) + 1;
             A->ticket[0] = 0;
             A->done[0] = 0;
-            // the last head task (done: every task has run) already published the flag
-            // to pose_host; a timeout must not leak into the next launch's waits
+            // the last head task already published the flag to pose_host; a timeout
+            // must not leak into the next launch's waits
             A->err[0] = 0;
-            // every read of the pushed frame and every pose store is done: tell the
-            // host (it spins on this word instead of waiting for the kernel's end)
-            __hip_atomic_store(A->done_host, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }

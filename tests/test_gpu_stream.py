@@ -155,3 +155,27 @@ def test_online_timeout_recovers():
         if i != 10 - s.h:
             assert np.abs(p - ref[i]).max() < 1e-5, i
     assert np.array_equal(s.run(seq), OnlineIK(m, use_graph=True).run(seq))
+
+
+@pytest.mark.parametrize("n_first", [7, 8])
+def test_online_reset_restores_the_activation_tag(n_first):
+    """The dataflow kernel hands activations over through the launch parity in
+    their sign bit (online.hip): launch c writes tag c & 1, and a consumer waits
+    for it. reset() restarts the frame count at 0, so it must also put every
+    element back to tag 1 — after an odd number of pushes the buffer holds tag 0,
+    which launch 0 would otherwise accept as fresh (stale rows, wrong poses)."""
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    r = golden("run_inference.npz")
+    seq = r["seq"][:30]
+    m = synthetic_model(win_size=64, device="cuda")
+    ref = OnlineIK(m, use_graph=True).run(seq)
+    s = OnlineIK(m, use_graph=True)
+    s.reset()
+    other = r["seq"][100:100 + n_first]
+    for fr in other:
+        s.push(fr)
+    # run() resets, then replays seq from frame 0
+    assert np.array_equal(s.run(seq), ref)

@@ -32,6 +32,7 @@
 // Every wait is bounded (0.5 s): a timeout sets *err and the task proceeds,
 // so the grid always drains; the host reports the error.
 #include "online.h"
+#include "xgemm_dev.h"
 
 namespace tik {
 
@@ -252,6 +253,13 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
 }
 
 // ---- T_L(t, 16 channels): out = ReLU(sum_tap z[s t + tap - 1] . wt_tap^T + bias + residual)
+// staged T row length (floats): the K range 3 C + cinp, or 32 K32 if longer, + 4
+// (an odd number of 16-B units: the 16 rows' ds_read_b128 hit distinct banks)
+__device__ __forceinline__ int onl_tconv_ld(int C, int cinp, int K32) {
+    const int k = 3 * C + cinp > 32 * K32 ? 3 * C + cinp : 32 * K32;
+    return k + 4;
+}
+
 // Staged operand rows, one per joint, in K order: [z tap 0 (C) | tap 1 | tap 2 | block
 // input x (cinp: the residual conv's K segment, or the identity term)], so K step sk
 // reads floats 4 sk .. of the row (no per-step tap decode between the MFMAs)
@@ -263,24 +271,36 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ksl = wave, kk = lane >> 4, ri = lane & 15;
     const int t = idx / ph.ngroups, cg = idx - t * ph.ngroups;
-    const int C = L.cout, C4 = C >> 2, K4t = 3 * C4, cinp4 = L.cinp >> 2;
+    const int C = L.cout, C4 = C >> 2, cinp4 = L.cinp >> 2;
     const bool rconv = L.res == ONR_CONV;
-    const int K4 = K4t + (rconv ? cinp4 : 0), c0 = cg * 16;
+    const int c0 = cg * 16;
     const int s = L.stride, tin = L.tin, fx = s * t;
-    const int LK = 3 * C + L.cinp + onl::LDP, LK4 = LK / 4;   // staged row (floats)
-    constexpr int NS = (3 * ONL_MAXC + ONL_MAXC) / 4 / ONL_KSL;   // K steps per wave (at most): 16
-    // this wave's weights: K step sk < K4t is tap sk / C4, channels 4 (sk % C4) ..; then the residual conv
-    float w[NS];
-    const float* wt = L.wt + (size_t)(c0 + ri) * 3 * C;
-    const float* wr = rconv ? L.wr + (size_t)(c0 + ri) * L.cinp : L.wt;
+    // K = 3 C (+ cinp: the residual conv) in steps of 32 (L.k32, zero-padded)
+    const int K32 = L.k32, Kt = 3 * C + (rconv ? L.cinp : 0);
+    const int LK = onl_tconv_ld(C, L.cinp, K32), LK4 = LK / 4;   // staged row (floats)
+    constexpr int NS = (4 * ONL_MAXC / 32 + ONL_KSL - 1) / ONL_KSL;   // K steps per wave (at most): 2
+    // this wave's weights: bf16x3 planes of K step sk (MFMA B operand: lane = channel
+    // c0 + (lane & 15), K 8 (lane >> 4) ..) and the same 8 fp32 values for joint 16
+    xbf16x8 w[NS][3];
+    f32x4 wf[NS][2];
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
         const int sk = ksl + ONL_KSL * q;
-        w[q] = sk < K4t ? wt[4 * sk + kk] : (sk < K4 ? wr[4 * (sk - K4t) + kk] : 0.f);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            w[q][pl] = sk < K32 ? *reinterpret_cast<const xbf16x8*>(L.wtp + ((((size_t)cg * K32 + sk) * 3 + pl) * 64 + lane) * 8)
+                                : xbf16x8{};
+        const float* wr = L.wtf + (size_t)(c0 + ri) * 32 * K32 + 32 * sk + 8 * kk;
+        wf[q][0] = sk < K32 ? *reinterpret_cast<const f32x4*>(wr) : f32x4{0.f, 0.f, 0.f, 0.f};
+        wf[q][1] = sk < K32 ? *reinterpret_cast<const f32x4*>(wr + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const float bt = L.biasT[c0 + (tid & 15)];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) onl_hold(w[q]);
+    for (int q = 0; q < NS; ++q) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+v"(w[q][pl]));
+        asm volatile("" : "+v"(wf[q][0]), "+v"(wf[q][1]));
+    }
     // staging: the block input rows (the previous layer's temporal conv, frame fx) and
     // the three z frames, every load in flight at once; each element is then polled
     // until it carries this launch's tag (usually only the newest frame's)
@@ -330,22 +350,42 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
             }
         }
     }
+    // the K padding past Kt (layer 0: 196 -> 224) reads zeros
+    for (int i = tid; i < 17 * (32 * K32 - Kt); i += onl::NT) {
+        const int v = i / (32 * K32 - Kt);
+        sm[v * LK + Kt + (i - v * (32 * K32 - Kt))] = 0.f;
+    }
     __syncthreads();
     if (tid == 0) onl_mark(A, task, 2);
     // identity residual of this thread's output (v = tid / 16, threads 0-271),
     // read before the reduction reuses the LDS
     const float res = (L.res == ONR_IDEN && tid < 272) ? sm[(tid >> 4) * LK + 3 * C + c0 + (tid & 15)] : 0.f;
-    const float* ra = sm + ri * LK + kk;
-    const float* r16 = sm + 16 * LK + kk;
-    // four independent accumulation chains (the MFMA's dependent latency), summed in a fixed order
+    // bf16x3 products on v_mfma_f32_16x16x32_bf16 (A = the staged rows, split into three
+    // bf16 planes in registers: lane = joint lane & 15, K 8 (lane >> 4) ..; six products,
+    // fp32 accumulation), joint 16 in fp32 FMAs
+    const float* ra = sm + ri * LK + 8 * kk;
+    const float* r16 = sm + 16 * LK + 8 * kk;
     onl_f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     float p16 = 0.f;
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
         const int sk = ksl + ONL_KSL * q;
-        if (sk < K4) {
-            acc[q & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[4 * sk], w[q], acc[q & 3], 0, 0, 0);
-            p16 = fmaf(r16[4 * sk], w[q], p16);
+        if (sk < K32) {
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(ra + 32 * sk), hi = *reinterpret_cast<const f32x4*>(ra + 32 * sk + 4);
+            xbf16x8 x0, x1, x2;
+            xsplit8(lo, hi, x0, x1, x2);
+            onl_f32x4& a0 = acc[2 * q], &a1 = acc[2 * q + 1];
+            a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, w[q][0], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, w[q][1], a1, 0, 0, 0);
+            a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[q][2], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, w[q][0], a1, 0, 0, 0);
+            a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[q][1], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[q][0], a1, 0, 0, 0);
+            const f32x4 l16 = *reinterpret_cast<const f32x4*>(r16 + 32 * sk), h16 = *reinterpret_cast<const f32x4*>(r16 + 32 * sk + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) p16 = fmaf(l16[e], wf[q][0][e], p16);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) p16 = fmaf(h16[e], wf[q][1][e], p16);
         }
     }
     const onl_f32x4 accs = (acc[0] + acc[1]) + (acc[2] + acc[3]);

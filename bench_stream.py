@@ -35,8 +35,8 @@ def measure_online(frames=10000, warmup=100, win=64, use_graph=True, precision="
     return {"metric": "online IK per-frame latency (p50)", "value": round(float(np.percentile(lat_us, 50)), 2),
             "unit": "us", "higher_is_better": False, "p99_us": round(float(np.percentile(lat_us, 99)), 2),
             "mean_us": round(float(lat_us.mean()), 2), "frames_per_s": round(frames / lat.sum(), 1),
-            "n_gpus": 1, "dtype": ("f32: temporal convs via bf16x3 MFMA (3 bf16 planes, 6 products, fp32 accumulate), gcn on exact fp32 MFMA, "
-                                             "head in fp32 FMAs") if s.path == "dataflow" else precision, "step": s.path,
+            "n_gpus": 1, "dtype": ("f32: gcn and temporal convs via bf16x3 MFMA (3 bf16 planes, 6 products, fp32 accumulate), "
+                                             "joint 16, graph mix and head in fp32 FMAs") if s.path == "dataflow" else precision, "step": s.path,
             "config": {"workload": f"stride-1 sliding window, win_size={win} (T={2 * (win // 2) + 1}), B=1, "
                                    f"{'hipGraph replay' if use_graph else 'eager launches'} per frame"
                                    + (" (one dataflow kernel, only the frames pose row 0 depends on)"

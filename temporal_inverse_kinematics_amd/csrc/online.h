@@ -34,6 +34,9 @@ struct OnlineLayer {
     int tin;           // the layer's real input frame count (zero padding past it)
     int n_in, n_out;   // frames computed: z (gcn) / out (temporal conv)
     const float *wg, *bias2, *amix, *wt, *wr, *biasT;   // the fp32 folded weights of api.cpp's Layer
+    int gk32;                    // gcn K = cinp in steps of 32
+    const unsigned short* wgp;   // gcn weight planes [cout/16][gk32][3][64][8] (stream-owned)
+    const float* wgf;            // gcn weights fp32, [cout][32 gk32] zero-padded (joint 16)
     int k32;                     // temporal conv K = 3 cout (+ cinp, residual conv) in steps of 32
     const unsigned short* wtp;   // its bf16x3 planes [cout/16][k32][3][64 lanes][8] (stream-owned)
     const float* wtf;            // the same weights fp32, [cout][32 k32] zero-padded (joint 16)

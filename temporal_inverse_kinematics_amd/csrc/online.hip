@@ -182,23 +182,27 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
     const int ksl = wave, kk = lane >> 4, ri = lane & 15;
     const int f = idx / ph.ngroups, cg = idx - f * ph.ngroups;
     const int cinp = L.cinp, K4 = cinp >> 2, cout = L.cout, c0 = cg * 16;
-    const int LD = cinp + onl::LDP;
-    constexpr int NS = ONL_MAXC / 4 / ONL_KSL;   // K steps per wave (at most)
-    static_assert(ONL_MAXC / 4 <= NS * ONL_KSL, "gcn K steps");
-    // operands that do not depend on the input: this wave's weight column, mix column, bias
-    float w[NS];
+    const int K32 = L.gk32;                                  // K = cinp in steps of 32 (zero-padded)
+    const int LD = (cinp > 32 * K32 ? cinp : 32 * K32) + 4;  // staged row: an odd number of 16-B units
+    static_assert(ONL_MAXC / 32 <= ONL_KSL, "gcn K steps: at most one per wave");
+    // operands that do not depend on the input: this wave's weight planes (bf16x3, MFMA B
+    // operand) and fp32 values (joint 16), mix column, bias
+    const int sk = ksl;
+    xbf16x8 w[3];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const int sk = ksl + ONL_KSL * q;
-        w[q] = sk < K4 ? L.wg[(size_t)(c0 + ri) * cinp + 4 * sk + kk] : 0.f;
-    }
+    for (int pl = 0; pl < 3; ++pl)
+        w[pl] = sk < K32 ? *reinterpret_cast<const xbf16x8*>(L.wgp + ((((size_t)cg * K32 + sk) * 3 + pl) * 64 + lane) * 8) : xbf16x8{};
+    const float* wgr = L.wgf + (size_t)(c0 + ri) * 32 * K32 + 32 * sk + 8 * kk;
+    f32x4 wf0 = sk < K32 ? *reinterpret_cast<const f32x4*>(wgr) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 wf1 = sk < K32 ? *reinterpret_cast<const f32x4*>(wgr + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     const int wo = tid >> 4, co = tid & 15;   // mix output (wo, co) of threads 0-271
     float am[17], b = 0.f;
 #pragma unroll
     for (int v = 0; v < 17; ++v) am[v] = tid < 272 ? L.amix[v * 17 + wo] : 0.f;
     if (tid < 272) b = L.bias2[wo * cout + c0 + co];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) onl_hold(w[q]);
+    for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+v"(w[pl]));
+    asm volatile("" : "+v"(wf0), "+v"(wf1));
     onl_hold(b);
 #pragma unroll
     for (int v = 0; v < 17; ++v) onl_hold(am[v]);
@@ -225,19 +229,33 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
             }
         }
     }
+    // the K padding past cinp (layer 0: 4 -> 32) reads zeros
+    for (int i = tid; i < 17 * (32 * K32 - cinp); i += onl::NT) {
+        const int v = i / (32 * K32 - cinp);
+        sm[v * LD + cinp + (i - v * (32 * K32 - cinp))] = 0.f;
+    }
     __syncthreads();
     if (tid == 0) onl_mark(A, task, 2);
-    const float* xa = sm + ri * LD + kk;
-    const float* x16 = sm + 16 * LD + kk;
+    // bf16x3 products on v_mfma_f32_16x16x32_bf16 (rows split into planes in registers), joint 16 in fp32 FMAs
     onl_f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     float p16 = 0.f;
+    if (sk < K32) {
+        const float* xa = sm + ri * LD + 32 * sk + 8 * kk;
+        const float* x16 = sm + 16 * LD + 32 * sk + 8 * kk;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(xa), hi = *reinterpret_cast<const f32x4*>(xa + 4);
+        xbf16x8 x0, x1, x2;
+        xsplit8(lo, hi, x0, x1, x2);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, w[0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, w[1], acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[2], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, w[0], acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[1], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, w[0], acc[1], 0, 0, 0);
+        const f32x4 l16 = *reinterpret_cast<const f32x4*>(x16), h16 = *reinterpret_cast<const f32x4*>(x16 + 4);
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const int sk = ksl + ONL_KSL * q;
-        if (sk < K4) {
-            acc[q & 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[4 * sk], w[q], acc[q & 1], 0, 0, 0);
-            p16 = fmaf(x16[4 * sk], w[q], p16);
-        }
+        for (int e = 0; e < 4; ++e) p16 = fmaf(l16[e], wf0[e], p16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) p16 = fmaf(h16[e], wf1[e], p16);
     }
     if (tid == 0) onl_mark(A, task, 3);
     onl_reduce_mfma(acc[0] + acc[1], p16, sm, true);

@@ -45,8 +45,8 @@ struct tik_stream {
     DevIBuf onl_cnt;                      // completion counters, ticket, done, err
     DevArray<tik::OnlineArgs> onl_args;   // the kernel's argument block
     DevArray<unsigned long long> onl_trace;   // TIK_ONLINE_TRACE=1
-    std::vector<DevHBuf> onl_wtp;         // per layer: temporal conv weights as bf16x3 MFMA planes
-    std::vector<DevBuf> onl_wtf;          // per layer: the same, fp32, K zero-padded to 32
+    std::vector<DevHBuf> onl_wtp, onl_wgp;   // per layer: temporal conv / gcn weights as bf16x3 MFMA planes
+    std::vector<DevBuf> onl_wtf, onl_wgf;    // per layer: the same, fp32, K zero-padded to 32
     int onl_ntasks = 0;
     ~tik_stream() {
         if (st) (void)hipStreamSynchronize(st);
@@ -75,21 +75,14 @@ static int setup_online(tik_stream* s) {
     // the temporal conv tasks' weights (online.hip onl_tconv): K = [tap 0 | tap 1 | tap 2 |
     // residual conv] per output channel, zero-padded to steps of 32, as bf16x3 planes in the
     // MFMA B-operand lane layout and as fp32 rows
-    s->onl_wtp.resize(nl);
-    s->onl_wtf.resize(nl);
-    for (int l = 0; l < nl; ++l) {
-        tik::OnlineLayer& L = a.L[l];
-        const int C = L.cout, cinp = L.cinp, rconv = L.res == tik::ONR_CONV;
-        const int Kt = 3 * C + (rconv ? cinp : 0), K32 = (Kt + 31) / 32;
-        std::vector<float> wt((size_t)C * 3 * C), wr(rconv ? (size_t)C * cinp : 0);
-        HIP_TRY(hipMemcpy(wt.data(), L.wt, wt.size() * sizeof(float), hipMemcpyDeviceToHost));
-        if (rconv) HIP_TRY(hipMemcpy(wr.data(), L.wr, wr.size() * sizeof(float), hipMemcpyDeviceToHost));
-        std::vector<float> wf((size_t)C * 32 * K32, 0.f);
-        for (int co = 0; co < C; ++co)
-            for (int k = 0; k < Kt; ++k)
-                wf[(size_t)co * 32 * K32 + k] = k < 3 * C ? wt[(size_t)co * 3 * C + k] : wr[(size_t)co * cinp + (k - 3 * C)];
-        std::vector<unsigned short> wp((size_t)(C / 16) * K32 * 3 * 64 * 8);
-        for (int cg = 0; cg < C / 16; ++cg)
+    s->onl_wtp.resize(nl); s->onl_wtf.resize(nl); s->onl_wgp.resize(nl); s->onl_wgf.resize(nl);
+    // rows [cout][Kt] -> fp32 rows zero-padded to K32 steps of 32 + bf16x3 planes [cout/16][K32][3][64][8]
+    auto pack = [](const std::vector<float>& w, int cout, int Kt, int K32, std::vector<float>& wf, std::vector<unsigned short>& wp) {
+        wf.assign((size_t)cout * 32 * K32, 0.f);
+        for (int co = 0; co < cout; ++co)
+            for (int k = 0; k < Kt; ++k) wf[(size_t)co * 32 * K32 + k] = w[(size_t)co * Kt + k];
+        wp.assign((size_t)(cout / 16) * K32 * 3 * 64 * 8, 0);
+        for (int cg = 0; cg < cout / 16; ++cg)
             for (int sk = 0; sk < K32; ++sk)
                 for (int ln = 0; ln < 64; ++ln)
                     for (int e = 0; e < 8; ++e) {
@@ -97,8 +90,24 @@ static int setup_online(tik_stream* s) {
                         split_bf16x3(wf[(size_t)(16 * cg + (ln & 15)) * 32 * K32 + 32 * sk + 8 * (ln >> 4) + e], h[0], h[1], h[2]);
                         for (int pl = 0; pl < 3; ++pl) wp[((((size_t)cg * K32 + sk) * 3 + pl) * 64 + ln) * 8 + e] = h[pl];
                     }
+    };
+    for (int l = 0; l < nl; ++l) {
+        tik::OnlineLayer& L = a.L[l];
+        const int C = L.cout, cinp = L.cinp, rconv = L.res == tik::ONR_CONV;
+        const int Kt = 3 * C + (rconv ? cinp : 0), K32 = (Kt + 31) / 32, G32 = (cinp + 31) / 32;
+        std::vector<float> wt((size_t)C * 3 * C), wr(rconv ? (size_t)C * cinp : 0), wg((size_t)C * cinp), w((size_t)C * Kt), wf;
+        std::vector<unsigned short> wp;
+        HIP_TRY(hipMemcpy(wt.data(), L.wt, wt.size() * sizeof(float), hipMemcpyDeviceToHost));
+        if (rconv) HIP_TRY(hipMemcpy(wr.data(), L.wr, wr.size() * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(wg.data(), L.wg, wg.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (int co = 0; co < C; ++co)
+            for (int k = 0; k < Kt; ++k) w[(size_t)co * Kt + k] = k < 3 * C ? wt[(size_t)co * 3 * C + k] : wr[(size_t)co * cinp + (k - 3 * C)];
+        pack(w, C, Kt, K32, wf, wp);
         if ((rc = s->onl_wtp[l].upload(wp)) || (rc = s->onl_wtf[l].upload(wf))) return rc;
         L.k32 = K32; L.wtp = s->onl_wtp[l].p; L.wtf = s->onl_wtf[l].p;
+        pack(wg, C, cinp, G32, wf, wp);
+        if ((rc = s->onl_wgp[l].upload(wp)) || (rc = s->onl_wgf[l].upload(wf))) return rc;
+        L.gk32 = G32; L.wgp = s->onl_wgp[l].p; L.wgf = s->onl_wgf[l].p;
     }
     int t = s->W;
     for (int l = 0; l < nl; ++l) {

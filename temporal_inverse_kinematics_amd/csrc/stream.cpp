@@ -299,9 +299,9 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
     }
     bool seen = false;
     if (s->online) {
-        // the dataflow kernel's last workgroup writes the new frame count to pinned
-        // host memory after the pose: spin on it (a few us sooner than the completion
-        // signal hipStreamSynchronize waits for); the stream stays ordered for the next step
+        // the dataflow kernel's last head task writes the new frame count to pinned
+        // host memory after the pose: spin on it (sooner than the completion signal
+        // hipStreamSynchronize waits for); the stream stays ordered for the next step
         const int want = (int)((s->pushed + 1) & 0x7fffffff);
         const auto t0 = std::chrono::steady_clock::now();
         for (long it = 0;; ++it) {

@@ -37,6 +37,12 @@ class OnlineIK:
         self._destroy = lib.tik_stream_destroy
         self._pose = np.zeros(66, np.float32)
         self._last = None
+        # per-push overhead: the frame goes through one preallocated buffer and both
+        # ctypes pointers are made once (building them per call cost ~8 us of a ~60 us push)
+        self._push_fn = lib.tik_stream_push
+        self._fbuf = np.zeros(51, np.float32)
+        self._fptr = self._fbuf.ctypes.data_as(_lib._F)
+        self._pptr = self._pose.ctypes.data_as(_lib._F)
         self.path = "dataflow" if _lib.check(lib.tik_stream_path(self._s)) == 1 else "layered"
 
     def __del__(self):
@@ -52,12 +58,14 @@ class OnlineIK:
 
     def push(self, frame: np.ndarray) -> Optional[np.ndarray]:
         """frame (17,3) -> the (66,) pose of the frame h pushes back, or None while filling."""
-        f = np.ascontiguousarray(frame, dtype=np.float32).reshape(-1)
+        f = np.asarray(frame, dtype=np.float32)
         if f.size != 51:
             raise ValueError("expected one (17,3) COCO frame")
-        self._last = f
-        rc = _lib.check(_lib.load().tik_stream_push(self._s, f.ctypes.data_as(_lib._F),
-                                                    self._pose.ctypes.data_as(_lib._F)), "OnlineIK.push")
+        self._fbuf[:] = f.reshape(-1)
+        self._last = self._fbuf   # the last pushed frame (flush repeats it)
+        rc = self._push_fn(self._s, self._fptr, self._pptr)
+        if rc < 0:
+            _lib.check(rc, "OnlineIK.push")
         return self._pose.copy() if rc == 1 else None
 
     def flush(self):

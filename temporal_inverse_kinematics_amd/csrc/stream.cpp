@@ -136,7 +136,7 @@ static int setup_online(tik_stream* s) {
     a.act = s->onl_act.p;
     a.act_bytes = (unsigned)(tot * sizeof(float));
     // every G / T output carries its launch's tag (online.hip): start at tag 1, for launch 0
-    HIP_TRY(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(s->onl_act.p), (int)0x80000000u, s->onl_act.n));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s->onl_act.p), (int)0x80000000u, s->onl_act.n, s->st));
     int np = 0, task = 0, cb = 0;
     auto add = [&](int kind, int layer, int nf, int ng) {
         a.ph[np++] = tik::OnlinePhase{kind, layer, nf, ng, task, cb};
@@ -151,7 +151,10 @@ static int setup_online(tik_stream* s) {
     a.nph = np;
     a.ntasks = task;
     if ((rc = s->onl_cnt.reserve(cb + 3))) return rc;
-    HIP_TRY(hipMemset(s->onl_cnt.p, 0, sizeof(int) * (cb + 3)));
+    HIP_TRY(hipMemsetAsync(s->onl_cnt.p, 0, sizeof(int) * (cb + 3), s->st));
+    // the initial tags and scheduling words are in place before the first step on this
+    // (non-blocking) stream: the memsets ran on it, and the host waits here
+    HIP_TRY(hipStreamSynchronize(s->st));
     a.cnt = s->onl_cnt.p; a.ncnt = cb;
     a.ticket = a.cnt + cb; a.done = a.cnt + cb + 1; a.err = a.cnt + cb + 2;
     a.ring = s->ring.p; a.W = s->W; a.h = s->h; a.ra = 11; a.rb = 12; a.relative = 1;

@@ -5,12 +5,12 @@
 // frame t of a stride-s layer reads input frames s*t-1 .. s*t+1. Walking that
 // back from the head gives each layer's needed frame count (n_out, n_in; 1,
 // 2, 4, 8, 9, 10, 20, 21, 22 input frames for the IK net at any window of at
-// least 22 frames). The step computes exactly those frames, in fp32 VALU
-// arithmetic, as a list of small tasks in topological order:
+// least 22 frames). The step computes exactly those frames as a list of small
+// tasks in topological order:
 //   G_L(f, 16 channels): gcn 1x1 conv + 17x17 graph mix + bias + ReLU (layer 0
 //          builds its input rows itself: window gather with the left-edge
 //          clamp, root-relative, data_bn; the pushed frame is read from pinned
-//          host memory and appended to the ring by the launch's last workgroup)
+//          host memory and appended to the ring by task 0)
 //   T_L(t, 16 channels): 3x1 temporal conv + residual + bias + ReLU
 //   H(16 hidden units + their share of the pose; the last H task sums the shares
 //          and writes the pose straight to pinned host memory)

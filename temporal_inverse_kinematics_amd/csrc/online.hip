@@ -2,9 +2,12 @@
 // kernel; see online.h for the task list and why only the first frames of
 // each layer are computed.
 //
-// Arithmetic: the gcn and temporal-conv tasks on the exact fp32 MFMA
-// (v_mfma_f32_16x16x4_f32: fp32 products, fp32 accumulation, like the
-// oracle); the head in fp32 VALU FMAs. Every task is one 1024-thread
+// Arithmetic: the gcn and temporal-conv tasks in bf16x3 on
+// v_mfma_f32_16x16x32_bf16 (the staged fp32 rows split into three bf16 planes
+// in registers, the weights pre-split per stream, six products, fp32
+// accumulation: fp32-class like the batch path; round 5 — the one-CU exact fp32
+// MFMA rate bounded the 256-channel tasks at 1.8 us); joint 16, the graph mix
+// and the head in fp32 VALU FMAs. Every task is one 1024-thread
 // workgroup (16 waves: 4 per SIMD, so LDS and memory latency overlap); the
 // task's weights are loaded into registers BEFORE it waits for its inputs,
 // and the input rows are staged into LDS with coalesced 16-B loads. A task's

@@ -5,9 +5,10 @@ solves a recorded sequence with one edge-padded window per frame. Online,
 frame c is solvable once frame c+h has arrived (h = win_size//2); each
 `push` appends a frame to a device ring, gathers the window centred h frames
 back and solves it (`tik_stream_*`). Output for frame c is identical to
-run_inference's. The default step is one dataflow kernel (csrc/online.hip)
-over only the frames pose row 0 depends on, in fp32 (`path == "dataflow"`);
-TIK_ONLINE=0 selects the layered forward over the whole window.
+run_inference's (within fp32 rounding). The default step is one dataflow
+kernel (csrc/online.hip) over only the frames pose row 0 depends on, its convs
+in bf16x3 MFMA arithmetic (`path == "dataflow"`); TIK_ONLINE=0 selects the
+layered forward over the whole window.
 """
 from __future__ import annotations
 

@@ -407,6 +407,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
+            "pose_rows_per_s": round(value * Tp, 1),   # windows/s x T' output rows
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

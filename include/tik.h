@@ -184,6 +184,10 @@ int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap);
  * 0.5 s wait timeout would; the next tik_stream_push then fails (that frame's
  * pose is invalid, the frame is still appended) and the one after it works. */
 int tik_debug_stream_inject_error(tik_stream_t s);
+/* Test hook: move the stream's frame count to `count`, which must be congruent to
+ * the current count modulo 2 * (2h + 1) (the same ring slot and launch parity),
+ * e.g. to just below the 2^30 wrap of stream_next_count (csrc/online.h). */
+int tik_debug_stream_set_count(tik_stream_t s, int count);
 
 /* ------------------------------------------------------------------------
  * Training-data generation (data half): AmassDataset

@@ -64,6 +64,7 @@ SIGNATURES: Dict[str, Tuple[object, Tuple]] = {
     "tik_train_windows": (_I, (_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _I, _I, ctypes.c_ulonglong, _P, _P, _P)),
     "tik_debug_stream_trace": (_I, (_P, ctypes.POINTER(ctypes.c_longlong), _I)),
     "tik_debug_stream_inject_error": (_I, (_P,)),
+    "tik_debug_stream_set_count": (_I, (_P, _I)),
     "tik_fk_create": (_I, (ctypes.POINTER(TikTensor), _I, _I, ctypes.POINTER(_P))),
     "tik_fk_destroy": (_I, (_P,)),
     "tik_fk_num_joints": (_I, (_P,)),

@@ -4,6 +4,7 @@
 //   * window gather              mmskeleton/datasets/data_amass.py:18-42, 221-236
 //   * generic ConvTemporalGraphical (reference NCTV layout)  gconv_origin.py:56-65
 #include "misc.h"
+#include "online.h"
 
 namespace tik {
 
@@ -179,7 +180,7 @@ __global__ void stream_push_kernel(float* ring, int W, int nv, int* count, const
     float* slot = ring + (size_t)(c % W) * nv;
     for (int i = threadIdx.x; i < nv; i += blockDim.x) slot[i] = frame[i];
     __syncthreads();
-    if (threadIdx.x == 0) *count = c + 1;
+    if (threadIdx.x == 0) *count = stream_next_count(c, W);
 }
 
 // window centred at c = count-1-h: frames c-h .. c+h = count-1-2h .. count-1,

@@ -23,6 +23,16 @@
 
 namespace tik {
 
+// The stream's frame count after one more push. It stays below 2^30: past it, a
+// multiple of 2W is subtracted (W = the odd ring size), which keeps the ring slot
+// (count % W), the launch parity (count & 1, online.hip's activation tag) and the
+// window's frame offsets, and stays far above the left-edge clamp (count >= 2^29).
+// Device kernels and the host's mirror of the count use the same rule.
+__host__ __device__ inline int stream_next_count(int c, int W) {
+    const int n = c + 1;
+    return n >= (1 << 30) ? n - 2 * W * ((1 << 29) / (2 * W)) : n;
+}
+
 constexpr int ONL_MAXL = 12;        // layers
 constexpr int ONL_MAXC = 256;       // channels per layer
 constexpr int ONL_MAXHC = 17;       // head K chunks of 4 per lane: K <= 17 * 4 * 64 = 4352 = 17 joints x ONL_MAXC

@@ -522,7 +522,7 @@ __device__ void onl_head(const OnlineArgs* __restrict__ A, int p, int idx, float
     // on the device and ordered before the next launch by the stream
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(A->done_host, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) __hip_atomic_store(A->done_host, stream_next_count(c, A->W), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restrict__ A) {
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(1024) void online_kernel(const OnlineArgs* __restri
         if (tid == 0) {
             // every task has read the count (the ring append and the host signal are
             // the last head task's)
-            A->count[0] = cnt_load(A->count) + 1;
+            A->count[0] = stream_next_count(cnt_load(A->count), A->W);
             A->ticket[0] = 0;
             A->done[0] = 0;
             // the last head task already published the flag to pose_host; a timeout

@@ -38,6 +38,7 @@ struct tik_stream {
     float* host_pose = nullptr;    // pinned; [pose_dim] = the online kernel's error flag
     volatile int* host_done = nullptr;   // pinned, coherent: the dataflow kernel's frame count after each step
     long long pushed = 0;
+    int dcount = 0;                       // mirror of the device frame count (stream_next_count)
     // the dataflow step (online.hip)
     bool online = false;
     int onl_grid = 0;
@@ -279,6 +280,7 @@ int tik_stream_reset(tik_stream_t s) {
     s->host_pose[s->pose_dim] = 0.f;
     *s->host_done = 0;
     s->pushed = 0;
+    s->dcount = 0;
     return TIK_OK;
 }
 
@@ -288,6 +290,18 @@ int tik_debug_stream_inject_error(tik_stream_t s) {
     const int one = 1;
     HIP_TRY(hipMemcpyAsync(s->onl_cnt.p + (s->onl_cnt.n - 1), &one, sizeof(int), hipMemcpyHostToDevice, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
+    return TIK_OK;
+}
+
+int tik_debug_stream_set_count(tik_stream_t s, int count) {
+    if (!s) return fail(TIK_E_INVALID, "null stream");
+    const long long period = 2LL * s->W;
+    if (count < 0 || count >= (1 << 30) || ((long long)count - s->dcount) % period != 0)
+        return fail(TIK_E_INVALID, "tik_debug_stream_set_count: %d is not the current count %d modulo %lld (or out of range)",
+                    count, s->dcount, period);
+    HIP_TRY(hipStreamSynchronize(s->st));
+    HIP_TRY(hipMemcpy(s->count.p, &count, sizeof(int), hipMemcpyHostToDevice));
+    s->dcount = count;
     return TIK_OK;
 }
 
@@ -305,7 +319,7 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
         // the dataflow kernel's last head task writes the new frame count to pinned
         // host memory after the pose: spin on it (sooner than the completion signal
         // hipStreamSynchronize waits for); the stream stays ordered for the next step
-        const int want = (int)((s->pushed + 1) & 0x7fffffff);
+        const int want = tik::stream_next_count(s->dcount, s->W);
         const auto t0 = std::chrono::steady_clock::now();
         for (long it = 0;; ++it) {
             if (*s->host_done == want) { seen = true; break; }
@@ -314,6 +328,7 @@ int tik_stream_push(tik_stream_t s, const float* frame_host, float* pose_host) {
     }
     if (!seen) HIP_TRY(hipStreamSynchronize(s->st));
     ++s->pushed;   // the step appended the frame to the device ring either way
+    s->dcount = tik::stream_next_count(s->dcount, s->W);
     if (s->online && s->host_pose[s->pose_dim] != 0.f) {
         s->host_pose[s->pose_dim] = 0.f;
         return fail(TIK_E_HIP, "tik_stream_push: the online kernel timed out waiting on a dependency "

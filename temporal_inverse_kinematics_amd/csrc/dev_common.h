@@ -18,6 +18,36 @@ __host__ __device__ constexpr unsigned coco_hop2_mask3(int w) {
     return m[w];
 }
 
+// ---- layer 0's spatial half, mix first: with C0 <= 4 input channels the
+// 17 x 17 graph mix commutes with the 1x1 conv (both linear; the conv bias is
+// inside bias2), so z[w] = bias2[w] + (sum_v A[v][w] x[v]) . Wg', mixing 4
+// channels once per (frame, joint) instead of 64 per output. Shared by the layered
+// kernel (layer0.hip) and the whole-block kernel (xblock.hip), which must agree
+// bit for bit. x4: the frame's 17 data_bn'd keypoints as 4 floats each (4th = 0);
+// amv: A_eff across the wave (lane l of amv[k] = A[64 k + l], v_readlane).
+template <bool SPARSE>
+__device__ __forceinline__ f32x4 l0_mix_in(const float* x4, const float (&amv)[5], int wj) {
+    f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < 17; ++v)
+        if (!SPARSE || ((coco_hop2_mask3(wj) >> v) & 1u)) {
+            const float av = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * 17 + wj) / 64]), (v * 17 + wj) % 64));
+            const f32x4 xv = *reinterpret_cast<const f32x4*>(x4 + 4 * v);
+            u = f32x4{fmaf(av, xv[0], u[0]), fmaf(av, xv[1], u[1]), fmaf(av, xv[2], u[2]), fmaf(av, xv[3], u[3])};
+        }
+    return u;
+}
+// the 1x1 conv of a mixed joint for 4 output channels + bias2, ReLU
+__device__ __forceinline__ f32x4 l0_conv_relu(const f32x4 u, const float (&w)[4][4], const f32x4 b) {
+    f32x4 z;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float s = fmaf(u[3], w[e][3], fmaf(u[2], w[e][2], fmaf(u[1], w[e][1], fmaf(u[0], w[e][0], b[e]))));
+        z[e] = s > 0.f ? s : 0.f;
+    }
+    return z;
+}
+
 // ---- buffer_load ... lds (raw buffer, stride 0): offsets at or past
 // num_records read as zeros, which implements every padded / out-of-range row
 typedef int i32x4 __attribute__((ext_vector_type(4)));

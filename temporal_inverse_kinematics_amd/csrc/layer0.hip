@@ -6,8 +6,10 @@
 // With C0 = 3 input channels the 1x1 conv is 3 MACs per output: a GEMM
 // (K padded to 32) would spend its MFMAs on zeros and force the input into a
 // padded 16-B-per-pixel operand.
-// Here each thread computes (frame, 4 output channels) for all 17 joints in
-// fp32 VALU: the kernel is bound by the z write (Cout x 4 B per pixel).
+// Here the graph mix runs first, on the 4-channel data_bn'd keypoints, once per
+// (frame, joint) (dev_common.h l0_mix_in), then each thread computes (frame, 4
+// output channels) for all 17 joints in fp32 VALU: bound by the z write
+// (Cout x 4 B per pixel).
 // Layer 0's residual conv (3 -> Cout) is folded into the temporal-conv
 // epilogue the same way (XArgs::rx: the data_bn'd keypoints as 16-B rows, xb4).
 #include "dev_common.h"
@@ -24,7 +26,7 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
     constexpr int VT = 17;
     const int G = Cout / 4;            // channel groups per frame
     const int FPB = 256 / G;           // frames per workgroup
-    __shared__ float xs[256 / 4 * VT * 4];   // up to 64 frames x 17 joints x 4 channels
+    __shared__ __attribute__((aligned(16))) float xs[256 / 4 * VT * 4];   // up to 64 frames x 17 joints x 4 channels
     const int tid = threadIdx.x;
     const int nframes = rows / VT;
     const int f0 = blockIdx.x * FPB;
@@ -44,6 +46,20 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
     for (int k = 0; k < NAM; ++k) amv[k] = 64 * k + (tid & 63) < VT * VT ? amix[64 * k + (tid & 63)] : 0.f;
     __syncthreads();
 
+    // mix first (dev_common.h l0_mix_in): u[f][w] for the block's frames x 17 joints,
+    // once each: wave wv takes the joints w = wv (mod 4) (wave-uniform, so the mix
+    // coefficients are v_readlane operands), lane = frame
+    __shared__ f32x4 us[256 / 4 * VT];
+    {
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), fl = tid & 63;
+        for (int fb = 0; fb < FPB; fb += 64)
+            if (fb + fl < FPB) {
+#pragma unroll
+                for (int wj = 0; wj < VT; ++wj)
+                    if ((wj & 3) == wv) us[(fb + fl) * VT + wj] = l0_mix_in<SPARSE != 0>(xs + (fb + fl) * VT * 4, amv, wj);
+            }
+    }
+    __syncthreads();
     const int f = tid / G, g = tid - f * G;
     const int frame = f0 + f;
     if (f >= FPB || frame >= nframes) return;
@@ -53,31 +69,13 @@ __global__ __launch_bounds__(256) void gcn0_kernel(const float* __restrict__ x, 
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int c = 0; c < 4; ++c) w[e][c] = c < C0 ? wg[(co + e) * ldwg + c] : 0.f;
-    f32x4 y[VT];
-#pragma unroll
-    for (int v = 0; v < VT; ++v) {
-        const float* xp = xs + (f * VT + v) * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[v][e] = xp[0] * w[e][0] + xp[1] * w[e][1] + xp[2] * w[e][2] + xp[3] * w[e][3];
-    }
     // all bias loads ahead of the stores
     f32x4 b[VT];
 #pragma unroll
     for (int wj = 0; wj < VT; ++wj) b[wj] = *reinterpret_cast<const f32x4*>(bias2 + wj * Cout + co);
 #pragma unroll
-    for (int wj = 0; wj < VT; ++wj) {
-        f32x4 z = b[wj];
-#pragma unroll
-        for (int v = 0; v < VT; ++v)
-            if (!SPARSE || ((coco_hop2_mask3(wj) >> v) & 1u)) {
-                const float av = __builtin_bit_cast(
-                    float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * VT + wj) / 64]), (v * VT + wj) % 64));
-                z += av * y[v];
-            }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
-        *reinterpret_cast<f32x4*>(out + ((size_t)frame * VT + wj) * ldo + co) = z;
-    }
+    for (int wj = 0; wj < VT; ++wj)
+        *reinterpret_cast<f32x4*>(out + ((size_t)frame * VT + wj) * ldo + co) = l0_conv_relu(us[f * VT + wj], w, b[wj]);
 }
 
 hipError_t launch_gcn0_f32(const float* x, int rows, int V, int C0, const float* bn_sc, const float* bn_sh,

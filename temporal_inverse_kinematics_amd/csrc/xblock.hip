@@ -46,7 +46,8 @@ constexpr int XBYTES = XINST * 1024;                   // 78,848 (padded to whol
 constexpr int B2BYTES = V * C * 4;                     // bias2 for the mix
 constexpr int KPBYTES = FIN * V * 4 * 4;               // RAW: data_bn'd keypoints, 4 floats per pixel
 constexpr int SMEM1 = ZBYTES + XBYTES + B2BYTES;       // block 1
-constexpr int SMEM0 = ZBYTES + KPBYTES;                // block 0
+constexpr int UBYTES = FIN * V * 16;                   // RAW: the mixed keypoints u[f][w] (4 floats)
+constexpr int SMEM0 = ZBYTES + KPBYTES + UBYTES;       // block 0
 constexpr int TPX = F * V, TBLK = (TPX + 15) / 16;     // 170 output pixels in 11 blocks of 16
 static_assert(SMEM1 <= 163840, "LDS");
 }  // namespace xb
@@ -212,8 +213,24 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             __syncthreads();
             stamp(0);
             if (tile + 1 < t_end) load_kp(tile + 1);   // lands under this tile's work
-            // thread (frame f, channel quad c4) of a joint half: waves 0-3 joints 0-8,
-            // waves 4-7 joints 9-16 (gcn0_kernel's arithmetic, layer0.hip)
+            // the graph mix first, on the 4-channel keypoints (dev_common.h l0_mix_in, as the
+            // layered gcn0_kernel): u[f][w] once per (frame, joint); wave wv takes the joints
+            // w = wv (mod 8) (wave-uniform: v_readlane coefficients), lane = frame
+            f32x4* const us = reinterpret_cast<f32x4*>(ximg + KPBYTES);
+            {
+                const int fl = lane;
+                if (fl < FIN) {
+#pragma unroll
+                    for (int wj = 0; wj < V; ++wj)
+                        if ((wj & 7) == wave) {
+                            if (a.mix_sparse) us[fl * V + wj] = l0_mix_in<true>(kps + fl * V * 4, amv, wj);
+                            else us[fl * V + wj] = l0_mix_in<false>(kps + fl * V * 4, amv, wj);
+                        }
+                }
+            }
+            __syncthreads();
+            // then the 1x1 conv + bias2 + ReLU, split into the z image: thread (frame f,
+            // channel quad c4) of a joint half: waves 0-3 joints 0-8, waves 4-7 joints 9-16
             const int f = tid & 15, c4 = (tid >> 4) & 15, half = wave >> 2, co = 4 * c4;
             if (f < FIN) {
                 float w[4][4];
@@ -221,28 +238,11 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
                     for (int c = 0; c < 4; ++c) w[e][c] = c < a.c0 ? a.wg0[(co + e) * a.ldwg0 + c] : 0.f;
-                f32x4 y[V];
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    const float* xp = kps + (f * V + v) * 4;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[v][e] = xp[0] * w[e][0] + xp[1] * w[e][1] + xp[2] * w[e][2] + xp[3] * w[e][3];
-                }
-                auto mix_half = [&](auto w0c, auto w1c, auto sparse) __attribute__((always_inline)) {
+                auto conv_half = [&](auto w0c, auto w1c) __attribute__((always_inline)) {
                     constexpr int W0 = decltype(w0c)::value, W1 = decltype(w1c)::value;
-                    constexpr bool SP = decltype(sparse)::value;
 #pragma unroll
                     for (int wj = W0; wj < W1; ++wj) {
-                        f32x4 z = *reinterpret_cast<const f32x4*>(a.bias2 + wj * C + co);
-#pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
-                                const float av = __builtin_bit_cast(
-                                    float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + wj) / 64]), (v * V + wj) % 64));
-                                z += av * y[v];
-                            }
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                        const f32x4 z = l0_conv_relu(us[f * V + wj], w, *reinterpret_cast<const f32x4*>(a.bias2 + wj * C + co));
                         // split into the three planes of z image row f * 17 + wj, channels co .. co + 3
                         xbf16x8 p0, p1, p2;
                         xsplit8(z, z, p0, p1, p2);
@@ -256,13 +256,8 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 using I0 = std::integral_constant<int, 0>;
                 using I9 = std::integral_constant<int, 9>;
                 using I17 = std::integral_constant<int, 17>;
-                if (half) {
-                    if (a.mix_sparse) mix_half(I9{}, I17{}, std::true_type{});
-                    else mix_half(I9{}, I17{}, std::false_type{});
-                } else {
-                    if (a.mix_sparse) mix_half(I0{}, I9{}, std::true_type{});
-                    else mix_half(I0{}, I9{}, std::false_type{});
-                }
+                if (half) conv_half(I9{}, I17{});
+                else conv_half(I0{}, I9{});
             }
         } else {
             // x image landed (every wave waits for its own DMA share, then the barrier)

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             constexpr int ZPF = 2, NS = 6 * NB;
             xbf16x8 zb[ZPF + 1][3];
             auto rdz = [&](int i, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
-                const int b = i / 6, s = i % 6, k = s >> 1, kb = s & 1;
+                const int b = i / 6, s = i % 6, k = s % 3, kb = s / 3;
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) d[pl] = *reinterpret_cast<const xbf16x8*>(zimg + xb_unit(rows[b][k], pl, 4 * kb + g));
             };
@@ -411,13 +411,13 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             for (int i = 0; i < ZPF; ++i) rdz(i, zb[i]);
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {   // K step s = (tap s / 2, K block s % 2): xgemm's K order
+            for (int i = 0; i < NS; ++i) {   // K step s = (K block s / 3, tap s % 3): xgemm's K order
                 const int b = i / 6, s = i % 6;
                 if (b >= nblk) break;
                 if (i + ZPF < NS) rdz(i + ZPF, zb[(i + ZPF) % (ZPF + 1)]);
                 __builtin_amdgcn_sched_barrier(0);
                 const xbf16x8(&z)[3] = zb[i % (ZPF + 1)];
-                const xbf16x8(&w)[3] = wt[s >> 1][s & 1];
+                const xbf16x8(&w)[3] = wt[s % 3][s / 3];
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], z[2], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], z[1], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], z[0], acc, 0, 0, 0);

@@ -13,7 +13,10 @@
 //
 // Contraction (same row conventions as cgemm.h): rows r = (n*tout + t')*V + w;
 // segment s, tap k reads source row (n*tin + stride*t' + k - pad)*V + w, zero
-// outside [0, tin). K step = (segment, tap, 32-channel block).
+// outside [0, tin). K step = (segment, 32-channel block, tap): the taps of a
+// block are adjacent, so the rows two taps share (stride 2: tap 2 of frame t is
+// tap 0 of frame t + 1) are re-read from L2 two steps later, not from MALL/HBM
+// a whole tap pass later.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     const i32x4 rB = buf_rsrc(a.wp, (unsigned)((size_t)gridDim.y * kall * C::BBYTES));
     const int nbw = (C::NIB_TOT - wave + NW - 1) / NW;   // this wave's B instructions per stage (NIBW or NIBW - 1)
 
-    // The A cursor walks (segment, tap, 32-channel block); segment slot 0 =
+    // The A cursor walks (segment, 32-channel block, tap); segment slot 0 =
     // seg[0], 1 = seg[1] (or the identity when nseg == 1), 2 = the identity.
     // The per-step advance reads the blocks and taps of each slot from one
     // packed 64-bit scalar (8 bits each; a select chain over separate values
@@ -180,26 +180,29 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
     auto advance_a = [&]() __attribute__((always_inline)) {
         const unsigned f = (unsigned)(nbkt >> (16 * ca_seg));
         ++ca_k;
-        if (++ca_blk >= (int)(f & 255u)) {
-            ca_blk = 0;
-            if (++ca_tap >= (int)((f >> 8) & 255u)) { ca_tap = 0; ++ca_seg; }
+        if (++ca_tap >= (int)((f >> 8) & 255u)) {   // taps innermost: a block's 3 taps read overlapping rows back to back
+            ca_tap = 0;
+            if (++ca_blk >= (int)(f & 255u)) { ca_blk = 0; ++ca_seg; }
         }
     };
-    unsigned a_off[NIA];
+    // per row, at the segment's change: its tap-0 input frame and byte offset;
+    // per step, tap k's offset is base + k frames, valid when the frame is in range
+    int a_t0[NIA], a_base[NIA];
+    int sg_tin = 0, sg_fb = 0, cur_seg = -1;   // the segment's frames, bytes per frame (V rows)
     i32x4 rA;
-    bool a_stale = true;   // a_off must be recomputed (a new tap or segment)
     auto prepare = [&]() __attribute__((always_inline)) {
-        if (!a_stale) return;
+        if (ca_seg == cur_seg) return;
+        cur_seg = ca_seg;
         const XSeg sg = ca_seg == 0 ? a.seg[0] : (ca_seg == 1 && two ? a.seg[1] : a.idn);
         rA = buf_rsrc(sg.src, (unsigned)(sg.rows_in * sg.ld * 4));
+        sg_tin = sg.tin;
+        sg_fb = V * sg.ld * 4;
 #pragma unroll
         for (int j = 0; j < NIA; ++j) {
-            const int t = sg.stride * a_t[j] + ca_tap - sg.pad;
-            a_off[j] = (a_ok[j] && t >= 0 && t < sg.tin)
-                           ? (unsigned)(((a_n[j] * sg.tin + t) * V + a_w[j]) * sg.ld * 4 + a_uo[j])
-                           : DMA_OOB;
+            const int t0 = sg.stride * a_t[j] - sg.pad;
+            a_t0[j] = a_ok[j] ? t0 : -(1 << 29);   // a dead row fails every tap
+            a_base[j] = ((a_n[j] * sg.tin + t0) * V + a_w[j]) * sg.ld * 4 + (int)a_uo[j];
         }
-        a_stale = false;
     };
     auto a_slot = [&](int s) __attribute__((always_inline)) { return smem + s * C::ABYTES; };
     auto b_slot = [&](int s) __attribute__((always_inline)) { return smem + NSA * C::ABYTES + s * C::BBYTES; };
@@ -207,12 +210,13 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         prepare();
         unsigned char* A = a_slot(ca_k % NSA);
         const int soA = __builtin_amdgcn_readfirstlane(ca_blk * 128);
+        const int tap = ca_tap, tb = tap * sg_fb;
         if (!(tune & 1))
 #pragma unroll
-            for (int j = 0; j < NIA; ++j) dma16(rA, A + (wave * NIA + j) * 1024, a_off[j], soA);
-        const int seg = ca_seg, tap = ca_tap;
+            for (int j = 0; j < NIA; ++j)
+                dma16(rA, A + (wave * NIA + j) * 1024,
+                      (unsigned)(a_t0[j] + tap) < (unsigned)sg_tin ? (unsigned)(a_base[j] + tb) : DMA_OOB, soA);
         advance_a();
-        a_stale = ca_seg != seg || ca_tap != tap;
     };
     auto issue_b = [&]() __attribute__((always_inline)) {   // weight step cb_k (main steps only)
         unsigned char* B = b_slot(cb_k % NSB);
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         nt = swz - (swz / ntn) * ntn;
     };
 
-    // ---- A cursor: tile ia, (segment, tap, block) within it, global step ga
+    // ---- A cursor: tile ia, (segment, block, tap) within it, global step ga
     int a_n[NIA], a_t[NIA], a_w[NIA], a_uo[NIA];
     bool a_ok[NIA];
 #pragma unroll
@@ -740,10 +744,10 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
         ++ga;
         const unsigned f = nbk >> (16 * ca_seg);
         const int seg = ca_seg, tap = ca_tap;
-        if (++ca_blk >= (int)(f & 255u)) {
-            ca_blk = 0;
-            if (++ca_tap >= (int)((f >> 8) & 255u)) {
-                ca_tap = 0;
+        if (++ca_tap >= (int)((f >> 8) & 255u)) {
+            ca_tap = 0;
+            if (++ca_blk >= (int)(f & 255u)) {
+                ca_blk = 0;
                 if (++ca_seg >= a.nseg) {   // the tile's last K step: on to the next tile
                     ca_seg = 0;
                     if (++ia < my) {
@@ -754,7 +758,7 @@ __global__ __launch_bounds__(256, 2) void xgemm_pt_kernel(XArgs a) {
                 }
             }
         }
-        a_stale = ca_seg != seg || ca_tap != tap || ca_blk == 0;
+        a_stale = ca_seg != seg || ca_tap != tap || (ca_blk == 0 && ca_tap == 0);
     };
     // ---- B cursor: tile ib (its column tile ntb), K step kbi, global step gb
     int ib = 0, kbi = 0, gb = 0, ntb;
@@ -1144,8 +1148,8 @@ std::vector<unsigned short> xgemm_pack(const XPackSeg* segs, int nseg, int Nc, i
         for (int s = 0; s < nseg; ++s) {
             const XPackSeg& sg = segs[s];
             const int nb = (sg.cin + 31) / 32;
-            for (int tap = 0; tap < sg.kt; ++tap)
-                for (int b = 0; b < nb; ++b, ++k) {
+            for (int b = 0; b < nb; ++b)
+                for (int tap = 0; tap < sg.kt; ++tap, ++k) {
                     unsigned short* base = out.data() + ((size_t)nt * ks + k) * tile;
                     for (int n = 0; n < bn; ++n) {
                         const int col = nt * bn + n;

@@ -33,8 +33,7 @@
 // every lane group (lanes of the two joints and the two frame halves land on
 // distinct 4-bank slots).
 // Products as xgemm (bf16x3, six products per K block), fp32 accumulation in
-// the order (K block, tap) — XT128 runs (tap, K block), so the two agree to
-// fp32 rounding of the accumulation order, not bit for bit.
+// the order (K block, tap), XT128's K order: the two are bitwise equal.
 #include <algorithm>
 #include <type_traits>
 

@@ -54,6 +54,11 @@ static_assert(SMEM1 <= 163840, "LDS");
 
 // unit u (16 B: 8 channels of one plane segment) of P3 image row R sits at u ^ (R & 7)
 __device__ __forceinline__ int xb_unit(int R, int plane, int u) { return R * xb::ROWB + plane * 128 + ((u ^ (R & 7)) << 4); }
+// block 1's x image (joint-major, row R = FIN j + f): unit u at u ^ ((R + j) & 7). Its G reads
+// (16 frames of one joint) stay conflict-free, and the residual reads (consecutive pixels: joints
+// j, j + 1, ... of one frame, rows FIN apart, which R & 7 put on 2 bank groups: 6x conflicts on
+// average) spread over all 8 units (1.9x)
+__device__ __forceinline__ int xb_xunit(int R, int j, int plane, int u) { return R * xb::ROWB + plane * 128 + ((u ^ ((R + j) & 7)) << 4); }
 
 template <bool RAW>
 __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             const int R = U / 24, k = U - R * 24, plane = k >> 3, up = k & 7;
             const int j = R / FIN, f = R - j * FIN, q = q0 - 1 + f;
             const bool ok = U < XUNITS && q >= 0 && q < QO;
-            const unsigned off = ok ? (unsigned)(((long long)q * V + j) * ROWB + plane * 128 + ((up ^ (R & 7)) << 4)) : DMA_OOB;
+            const unsigned off = ok ? (unsigned)(((long long)q * V + j) * ROWB + plane * 128 + ((up ^ ((R + j) & 7)) << 4)) : DMA_OOB;
             dma16(rX, ximg + ins * 1024, off, 0);
         }
     };
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 auto rd = [&](int s, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
                     const int R = (s >> 1) * FIN + fr, kb = s & 1;
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(ximg + xb_unit(R, p, 4 * kb + g));
+                    for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(ximg + xb_xunit(R, s >> 1, p, 4 * kb + g));
                 };
 #pragma unroll
                 for (int s = S0; s < S0 + XPF; ++s) rd(s, xb[(s - S0) % (XPF + 1)]);
@@ -366,9 +371,9 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
                 } else {
                     const int R = jt * FIN + fo + 1, u = cho >> 3, o = (cho & 7) * 2;
                     typedef __bf16 xbf16x4 __attribute__((ext_vector_type(4)));
-                    const xbf16x4 h0 = *reinterpret_cast<const xbf16x4*>(ximg + xb_unit(R, 0, u) + o);
-                    const xbf16x4 h1 = *reinterpret_cast<const xbf16x4*>(ximg + xb_unit(R, 1, u) + o);
-                    const xbf16x4 h2 = *reinterpret_cast<const xbf16x4*>(ximg + xb_unit(R, 2, u) + o);
+                    const xbf16x4 h0 = *reinterpret_cast<const xbf16x4*>(ximg + xb_xunit(R, jt, 0, u) + o);
+                    const xbf16x4 h1 = *reinterpret_cast<const xbf16x4*>(ximg + xb_xunit(R, jt, 1, u) + o);
+                    const xbf16x4 h2 = *reinterpret_cast<const xbf16x4*>(ximg + xb_xunit(R, jt, 2, u) + o);
 #pragma unroll
                     for (int e = 0; e < 4; ++e) res[b][e] = ((float)h0[e] + (float)h1[e]) + (float)h2[e];   // exact: x = p0 + p1 + p2
                 }

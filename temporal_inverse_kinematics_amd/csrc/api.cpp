@@ -599,7 +599,7 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     const HostTensor* W3 = find(m, "pose_regressor.3.weight");
     const HostTensor* B3 = find(m, "pose_regressor.3.bias");
     md->feat = V * cin;
-    md->prec = default_precision();
+    if ((rc = precision_from_env(md->prec))) { delete md; return rc; }
     if (!W0 && !B0 && !W3 && !B3) {
         // backbone-only handle (StgGcn18 state dict, st_gcn_aaai18.py:32-133):
         // tik_backbone_forward only; tik_ik_forward refuses it
@@ -616,7 +616,6 @@ int tik_model_create(const tik_tensor* tensors, int n_tensors, tik_model_t* out)
     md->pose_dim = (int)W3->shape[0];
     if ((int)W0->shape[1] != md->feat || (int)W3->shape[1] != md->hidden) { delete md; return fail(TIK_E_INVALID, "head shapes do not match backbone features %d", md->feat); }
     if (md->hidden % 4) { delete md; return fail(TIK_E_INVALID, "hidden size must be a multiple of 4"); }
-    md->prec = default_precision();
     if ((rc = md->trash.upload(std::vector<unsigned short>(4096, 0)))) {
         delete md;
         return rc;
@@ -1078,8 +1077,9 @@ int tik_block_create(const tik_tensor* tensors, int n_tensors, int in_channels, 
     TensorMap m = to_map(tensors, n_tensors);
     auto* b = new tik_block();
     std::vector<float> Ae(A_eff_host, A_eff_host + V * V);
-    b->prec = default_precision();
-    int rc = b->layer.build(m, "", in_channels, out_channels, stride, residual, Ae, V);
+    int rc = precision_from_env(b->prec);
+    if (rc) { delete b; return rc; }
+    rc = b->layer.build(m, "", in_channels, out_channels, stride, residual, Ae, V);
     if (rc) { delete b; return rc; }
     *out = b;
     return TIK_OK;

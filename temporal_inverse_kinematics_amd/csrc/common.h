@@ -180,12 +180,18 @@ struct SplitW3 {
 };
 
 // default arithmetic of the GEMMs (cgemm.h PREC_*): TIK_PRECISION=fp32 the
-// exact f32 MFMA path; default bf16x3, the 6-product bf16 split with fp32's
-// exponent range
-inline int default_precision() {
+// exact f32 MFMA path; unset or bf16x3, the 6-product bf16 split with fp32's
+// exponent range. Any other value fails the handle's creation (f16x3 was
+// retired in round 5: silently mapping it to bf16x3 would change the
+// arithmetic without a word)
+inline int precision_from_env(int& prec) {
     const char* e = getenv("TIK_PRECISION");
-    if (e && (std::string(e) == "fp32" || std::string(e) == "f32")) return 0;
-    return 2;
+    const std::string s = e ? e : "";
+    if (s.empty() || s == "bf16x3") prec = 2;
+    else if (s == "fp32" || s == "f32") prec = 0;
+    else if (s == "f16x3") return fail(TIK_E_INVALID, "TIK_PRECISION=f16x3 was retired (round 5); use bf16x3 or fp32");
+    else return fail(TIK_E_INVALID, "TIK_PRECISION=%s: expected bf16x3 or fp32", s.c_str());
+    return TIK_OK;
 }
 
 // One set of activation buffers for the IK forward. A model handle owns two

@@ -192,7 +192,7 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         if ((int)pm->v.size() != NJ * 3) return bad("pose_mean must be (55,3)");
         hpm = pm->v;
     }
-    fk->prec = default_precision();
+    if ((rc = precision_from_env(fk->prec))) { delete fk; return rc; }
     if ((rc = fk->PT.upload(PT)) || (rc = fk->WT.upload(WT)) || (rc = fk->jt.upload(jt)) || (rc = fk->jd.upload(jd)) ||
         (rc = fk->pose_mean.upload(hpm)) || (rc = fk->lmk_bary.upload(lb->v)) || (rc = fk->parents.upload(hpar)) ||
         (rc = fk->chain.upload(chain)) || (rc = fk->faces.upload(hfaces)) || (rc = fk->lmk_faces.upload(hlf)) ||

@@ -122,7 +122,7 @@ __device__ __forceinline__ float fma4(const float4 a, const float4 b, float c) {
 // (no input task, no round trip): window gather with the left-edge clamp,
 // root-relative, data_bn -> 17 rows of 4 floats at dst, row stride ld4 float4s (threads 0-16).
 // The pushed frame is read from pinned host memory; older frames from the ring,
-// which the last workgroup of the launch appends the pushed frame to.
+// which task 0 of the launch appends the pushed frame to (online_kernel).
 __device__ void onl_raw_rows(const OnlineArgs* __restrict__ A, int k, float4* dst, int ld4) {
     const int v = threadIdx.x;
     if (v >= 17) return;
@@ -141,14 +141,16 @@ __device__ void onl_raw_rows(const OnlineArgs* __restrict__ A, int k, float4* ds
     dst[v * ld4] = make_float4(o[0], o[1], o[2], 0.f);
 }
 
-// MFMA roles of a G / T task: wave w takes the K steps (4 input channels each)
-// w, w + 16, ... One v_mfma_f32_16x16x4_f32 per step covers joints 0-15: A = the
-// staged rows (lane: joint l & 15, K element l >> 4), B = the weights (lane: output
-// channel c0 + (l & 15), K element l >> 4), D lane l = joints 4 (l >> 4) + e,
-// channel c0 + (l & 15). Joint 16 is one VALU FMA per step on the same B register
-// (lane: channel l & 15, K element l >> 4), its 4 K elements summed across the
-// lane groups before the wave's partials go to LDS (a second 16-row MFMA block
-// for one joint would double the MFMA time).
+// MFMA roles of a G / T task: wave w takes the K steps (32 input channels each)
+// w, w + 16, ... Per step, six bf16x3 products on v_mfma_f32_16x16x32_bf16 cover
+// joints 0-15: A = the staged fp32 rows split into three bf16 planes in registers
+// (lane: joint l & 15, K elements 8 (l >> 4) .. + 7), B = the host-split weight
+// planes (lane: output channel c0 + (l & 15), the same K elements), D lane l =
+// joints 4 (l >> 4) + e, channel c0 + (l & 15). Joint 16 is 8 fp32 FMAs per step
+// on the fp32 copy of the same weights (lane: channel l & 15, K elements 8 (l >> 4)
+// ..), its 4 lane-group partials summed across the lane groups before the wave's
+// partials go to LDS (a second 16-row MFMA block for one joint would double the
+// MFMA time).
 typedef float onl_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int ONL_KSL = 16;   // K slices (one per wave)
 
@@ -274,16 +276,22 @@ __device__ void onl_gcn(const OnlineArgs* __restrict__ A, int p, int idx, float*
 }
 
 // ---- T_L(t, 16 channels): out = ReLU(sum_tap z[s t + tap - 1] . wt_tap^T + bias + residual)
-// staged T row length (floats): the K range 3 C + cinp, or 32 K32 if longer, + 4
-// (an odd number of 16-B units: the 16 rows' ds_read_b128 hit distinct banks)
-__device__ __forceinline__ int onl_tconv_ld(int C, int cinp, int K32) {
-    const int k = 3 * C + cinp > 32 * K32 ? 3 * C + cinp : 32 * K32;
+// where the block input x sits in a staged T row: at 3 C for the residual conv (its K
+// segment), past the K padding 32 K32 for the identity term (inside [3 C, 32 K32) the
+// padding is zeroed; C % 32 == 16 puts 16 floats of padding there)
+__device__ __forceinline__ int onl_tconv_xoff(int C, bool rconv, int K32) {
+    return rconv || 32 * K32 < 3 * C ? 3 * C : 32 * K32;
+}
+// staged T row length (floats): the K range and the staged x, + 4 (an odd number of
+// 16-B units: the 16 rows' ds_read_b128 hit distinct banks)
+__device__ __forceinline__ int onl_tconv_ld(int xoff, int cinp, int K32) {
+    const int k = xoff + cinp > 32 * K32 ? xoff + cinp : 32 * K32;
     return k + 4;
 }
 
 // Staged operand rows, one per joint, in K order: [z tap 0 (C) | tap 1 | tap 2 | block
-// input x (cinp: the residual conv's K segment, or the identity term)], so K step sk
-// reads floats 4 sk .. of the row (no per-step tap decode between the MFMAs)
+// input x (cinp: the residual conv's K segment, or the identity term past the K padding)],
+// so K step sk reads floats 4 sk .. of the row (no per-step tap decode between the MFMAs)
 __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, float* sm, int task, const unsigned E) {
     const OnlinePhase& ph = A->ph[p];
     const OnlineLayer& L = A->L[ph.layer];
@@ -298,7 +306,8 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     const int s = L.stride, tin = L.tin, fx = s * t;
     // K = 3 C (+ cinp: the residual conv) in steps of 32 (L.k32, zero-padded)
     const int K32 = L.k32, Kt = 3 * C + (rconv ? L.cinp : 0);
-    const int LK = onl_tconv_ld(C, L.cinp, K32), LK4 = LK / 4;   // staged row (floats)
+    const int XO = onl_tconv_xoff(C, rconv, K32), XO4 = XO / 4;   // staged block input (floats)
+    const int LK = onl_tconv_ld(XO, L.cinp, K32), LK4 = LK / 4;   // staged row (floats)
     constexpr int NS = (4 * ONL_MAXC / 32 + ONL_KSL - 1) / ONL_KSL;   // K steps per wave (at most): 2
     // this wave's weights: bf16x3 planes of K step sk (MFMA B operand: lane = channel
     // c0 + (lane & 15), K 8 (lane >> 4) ..) and the same 8 fp32 values for joint 16
@@ -348,13 +357,13 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
             if (live && i < nz) rz[tap][j] = ld4raw(ab, L.z + ((size_t)fr * nz + i) * 4);
         }
     }
-    if (L.res != ONR_ZERO && ph.layer == 0) onl_raw_rows(A, fx, s4 + 3 * C4, LK4);
+    if (L.res != ONR_ZERO && ph.layer == 0) onl_raw_rows(A, fx, s4 + XO4, LK4);
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
         const int i = tid + j * onl::NT;
         if (xin && i < 17 * cinp4) {
             const int v = i / cinp4;
-            s4[v * LK4 + 3 * C4 + (i - v * cinp4)] = onl_fin4(A, ab, xrow + 4 * i, E, rx[j]);
+            s4[v * LK4 + XO4 + (i - v * cinp4)] = onl_fin4(A, ab, xrow + 4 * i, E, rx[j]);
         }
     }
 #pragma unroll
@@ -371,7 +380,7 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
             }
         }
     }
-    // the K padding past Kt (layer 0: 196 -> 224) reads zeros
+    // the K padding past Kt (layer 0: 196 -> 224) reads zeros (disjoint from the staged x)
     for (int i = tid; i < 17 * (32 * K32 - Kt); i += onl::NT) {
         const int v = i / (32 * K32 - Kt);
         sm[v * LK + Kt + (i - v * (32 * K32 - Kt))] = 0.f;
@@ -380,7 +389,7 @@ __device__ void onl_tconv(const OnlineArgs* __restrict__ A, int p, int idx, floa
     if (tid == 0) onl_mark(A, task, 2);
     // identity residual of this thread's output (v = tid / 16, threads 0-271),
     // read before the reduction reuses the LDS
-    const float res = (L.res == ONR_IDEN && tid < 272) ? sm[(tid >> 4) * LK + 3 * C + c0 + (tid & 15)] : 0.f;
+    const float res = (L.res == ONR_IDEN && tid < 272) ? sm[(tid >> 4) * LK + XO + c0 + (tid & 15)] : 0.f;
     // bf16x3 products on v_mfma_f32_16x16x32_bf16 (A = the staged rows, split into three
     // bf16 planes in registers: lane = joint lane & 15, K 8 (lane >> 4) ..; six products,
     // fp32 accumulation), joint 16 in fp32 FMAs

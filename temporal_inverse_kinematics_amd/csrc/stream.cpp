@@ -263,6 +263,10 @@ int tik_stream_path(tik_stream_t s) {
 int tik_debug_stream_trace(tik_stream_t s, long long* out, int cap) {
     if (!s || !s->online || !s->onl_trace.p) return fail(TIK_E_INVALID, "no online trace (TIK_ONLINE_TRACE=1 at tik_stream_create)");
     const int n = std::min(cap / 8, s->onl_ntasks);
+    // a push returns once the pose is in host memory, while the launch's tail (the last
+    // tasks' end marks, the scheduling bookkeeping) may still run on the non-blocking
+    // stream, which a null-stream copy does not wait for
+    HIP_TRY(hipStreamSynchronize(s->st));
     if (out && n > 0) HIP_TRY(hipMemcpy(out, s->onl_trace.p, sizeof(long long) * 8 * n, hipMemcpyDeviceToHost));
     return s->onl_ntasks;
 }

@@ -37,6 +37,94 @@ def online_flag(_):
     return os.environ.get("TIK_ONLINE", "1") != "0"
 
 
+def test_online_default_path_win64_full_sample_vs_golden():
+    """the default online path (dataflow kernel, hipGraph
+    replay) over the whole 231-frame sample at win_size 64 (T = 65) against the
+    reference's own run_inference output (golden run_inference.npz:win64,
+    inference.py:37-67 over data_amass.py:18-42 windows) at 1e-4."""
+    import os
+    assert os.environ.get("TIK_ONLINE", "1") != "0"
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    r = golden("run_inference.npz")
+    assert r["seq"].shape[0] == 231
+    m = synthetic_model(win_size=64, device="cuda")
+    online = OnlineIK(m, use_graph=True)
+    assert online.path == "dataflow" and online.win_size == 64
+    got = online.run(r["seq"])
+    assert got.shape == r["win64"].shape == (231, 66)
+    assert np.abs(got - r["win64"]).max() < 1e-4
+
+
+def _regressor_with_layers(layers, win, seed=7):
+    """An IKPoseTrainer whose backbone has the given (cout, stride) blocks
+    (the last one 256 channels for the 17 x 256 head), seeded synthetic weights."""
+    import torch
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    from temporal_inverse_kinematics_amd.models import IKPoseTrainer, PoseRegressor, default_hparams
+
+    class Reg(PoseRegressor):
+        LAYERS = layers
+
+    class Trainer(IKPoseTrainer):
+        def __init__(self, hp):
+            torch.nn.Module.__init__(self)
+            self.hparams = hp
+            self.regressor = Reg(hp)
+
+    model = Trainer(default_hparams(win))
+    full, c = [], 3
+    for cout, s in layers:
+        full.append((c, cout, s))
+        c = cout
+    sd = syn.ik_state_dict(model.regressor.backbone.graph.A, seed=seed, layers=full)
+    res = model.regressor.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not [k for k in res.missing_keys if "num_batches_tracked" not in k] and not res.unexpected_keys
+    return model.cuda().eval()
+
+
+@pytest.mark.parametrize("c1", [48, 80])
+def test_online_identity_block_c_mod_32_eq_16(c1, monkeypatch):
+    """in the dataflow kernel's temporal-conv task the block
+    input x of an identity-residual layer is staged after the 3 C tap channels,
+    and the K padding up to a multiple of 32 is zeroed. With C % 32 == 16
+    (C = 48: 3 C = 144 -> 160) that padding overlapped x's first 16 channels,
+    so the identity term read zeros. x now sits past the padding. Both identity
+    blocks (layers 1 and 2) have C % 32 == 16; the dataflow step must equal the
+    layered one (TIK_ONLINE=0)."""
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.streaming import OnlineIK
+    layers = [(c1, 1), (c1, 1), (c1, 1), (128, 2), (128, 1), (128, 2), (256, 2), (256, 2)]
+    m = _regressor_with_layers(layers, 64)
+    seq = golden("run_inference.npz")["seq"][:40]
+    monkeypatch.setenv("TIK_ONLINE", "0")
+    ref = OnlineIK(m, use_graph=True).run(seq)
+    monkeypatch.setenv("TIK_ONLINE", "1")
+    s = OnlineIK(m, use_graph=True)
+    assert s.path == "dataflow"
+    got = s.run(seq)
+    assert np.isfinite(ref).all()
+    assert np.abs(got - ref).max() < 2e-5
+
+
+@pytest.mark.parametrize("value", ["f16x3", "bf16", "FP32"])
+def test_unknown_precision_env_fails(value, monkeypatch):
+    """an unrecognised TIK_PRECISION (the retired f16x3
+    included) fails the handle's creation instead of running bf16x3 silently."""
+    import torch
+    from temporal_inverse_kinematics_amd import _build
+    _build.build()
+    from temporal_inverse_kinematics_amd.inference import synthetic_model
+    monkeypatch.setenv("TIK_PRECISION", value)
+    m = synthetic_model(win_size=9, device="cuda")
+    with pytest.raises(Exception, match="TIK_PRECISION"):
+        with torch.no_grad():
+            m(torch.zeros(1, 9, 17, 3, device="cuda"))
+
+
 @pytest.mark.parametrize("win", [3, 21, 22, 23, 40, 64, 129])
 def test_online_kernel_matches_layered(win, monkeypatch):
     """The dataflow step (only the frames pose row 0 depends on, fp32) against

@@ -54,7 +54,9 @@ def kernel_symbol(label, precision):
     if label == "XGW":
         return "tik::xgraph_kernel"   # <K blocks, passes>: the label does not say which (any instantiation)
     if label == "XTW":
-        return "tik::xtws_kernel"
+        return "tik::xtws_kernel<1, 8, false>"
+    if label == "XTWG":   # xtws + the next block's gcn (FG)
+        return "tik::xtws_kernel<1, 8, true>"
     p = PREC_CODE[precision]
     nb_graph = 2 if p == 0 else 1
     cg = {"G272x64": f"272, 64, 1, 4, 1, 17, {p}, {nb_graph}", "T128x128": f"128, 128, 2, 2, 0, 0, {p}, 2",

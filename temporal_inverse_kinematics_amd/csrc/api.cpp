@@ -196,6 +196,7 @@ struct Layer {
     int xg_bn = 0, xt_bn = 0, xg_ks = 0, xt_ks = 0;
     int xgwon = 1;          // gcn on xgraph.hip where packed (TIK_XGW bit mask of layers; 0 = the XG tiles)
     int xtwson = 1;         // temporal conv on xtws.hip where packed (TIK_XTWS bit mask of layers; 0 = XT128)
+    int xfgon = 1;          // the next block's gcn inside this block's xtws launch where possible (TIK_XFG bit mask)
     float* xtrash = nullptr;   // store target of rows past M (persistent kernel), owned by the model
     bool mix_sparse = false;
 
@@ -347,17 +348,33 @@ struct Layer {
 
     bool x_ok() const { return xt.p && (xg.p || (index == 0 && cin <= 4 && res == RES_CONV && wr0.p)); }
 
+    // the temporal conv runs on xtws.hip (input rows x of ld floats, tin frames per window)
+    bool xtws_path(bool raw, int ld, int tin) const {
+        return xtwson && xtw.p && xtrash && !raw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0;
+    }
+    // block `nx`'s spatial half can run inside this block's xtws launch (xtws.hip FG:
+    // 128 -> 128 gcn planes on xgraph.hip's layout; TIK_XFG bit mask of this layer)
+    bool fuses_gcn_of(const Layer& nx) const {
+        return xfgon && xtw.p && nx.xgwon && nx.xgw.p && nx.cin == cout && cout == 128 && nx.cout == 128 && nx.V == 17;
+    }
+
     // bf16x3 on fp32 activations (xgemm.hip). x: fp32 rows [N*tin*V][ld];
     // z: workspace; out: [N*tout*V][cout]. Layer 0 from the raw keypoints
     // (cin <= 4): xraw = (N,T,V,C0) keypoints, its data_bn'd copy goes to xb4
     // ([rows][4]) for the residual conv in the temporal conv's epilogue.
+    //
+    // zin: this block's z, already made by the previous block's fused launch (no G
+    // launch here); gn / zn: the next block, whose z this block's xtws launch makes
+    // into zn (fuses_gcn_of(*gn) and xtws_path; the caller checks both)
     int forward_x(const float* x, int ld, int N, int tin, float* z, float* out, hipStream_t st, int ncu,
                   const float* xraw = nullptr, const float* bn_sc = nullptr, const float* bn_sh = nullptr,
-                  float* xb4 = nullptr) const {
+                  float* xb4 = nullptr, const float* zin = nullptr, const Layer* gn = nullptr, float* zn = nullptr) const {
         const int to = tout(tin, stride);
         const long long rin = (long long)N * tin * V, rout = (long long)N * to * V;
         const double px_in = (double)rin, px_out = (double)rout;
-        if (xraw) {
+        if (zin) {
+            z = const_cast<float*>(zin);
+        } else if (xraw) {
             ProfScope p("G0f_raw.L0", 2.0 * px_in * cin * cout + 2.0 * V * px_in * cout, 4.0 * (px_in * cin + px_in * cout), st);
             HIP_TRY(tik::launch_gcn0_f32(xraw, (int)rin, V, cin, bn_sc, bn_sh, wg.p, cinp, bias2.p, amix.p, mix_sparse ? 1 : 0,
                                          cout, z, cout, xb4, st));
@@ -384,13 +401,19 @@ struct Layer {
             p.out(z, (size_t)rin * cout * 4);
             HIP_TRY(launch_xgemm_traced(g, xg_bn, tik::EPI_GRAPH, st, lab.c_str()));
         }
-        if (xtwson && xtw.p && xtrash && !xraw && res == RES_IDEN && stride == 1 && ld >= cout && ld % 4 == 0 && tin % 8 == 0) {
+        if (xtws_path(xraw != nullptr, ld, tin)) {
             tik::XTConvArgs c{};
             c.M = (int)rout; c.T = tin; c.z = z; c.ldz = cout; c.x = x; c.ldx = ld; c.wp = xtw.p; c.bias = biasT.p;
             c.out = out; c.ldo = cout; c.nts = 1; c.trash = xtrash;
-            const std::string lab = "XTW.L" + std::to_string(index);
-            ProfScope p(lab.c_str(), 2.0 * px_out * TK * cout * cout,
-                        4.0 * (px_in * cout + 2.0 * px_out * cout + (double)TK * cout * cout), st);
+            double fl = 2.0 * px_out * TK * cout * cout, by = 4.0 * (px_in * cout + 2.0 * px_out * cout + (double)TK * cout * cout);
+            if (gn) {   // + block l+1's gcn: its algorithmic FLOPs, its z written (out is not re-read)
+                c.wg = gn->xgw.p; c.bias2 = gn->bias2.p; c.amix = gn->amix.p; c.mix_sparse = gn->mix_sparse ? 1 : 0;
+                c.zout = zn; c.ldzo = gn->cout;
+                fl += 2.0 * px_out * gn->cin * gn->cout + 2.0 * V * px_out * gn->cout;
+                by += 4.0 * (px_out * gn->cout + (double)gn->cout * gn->cin + (double)V * (V + gn->cout));
+            }
+            const std::string lab = (gn ? "XTWG.L" : "XTW.L") + std::to_string(index);
+            ProfScope p(lab.c_str(), fl, by, st);
             p.out(out, (size_t)rout * cout * 4);
             HIP_TRY(tik::launch_xtws(c, ncu, st));
             return TIK_OK;
@@ -491,6 +514,7 @@ static void apply_env(tik_model* md) {
     for (auto& L : md->layers) {
         if (const char* w = getenv("TIK_XGW")) L.xgwon = (atoi(w) >> L.index) & 1;
         if (const char* w = getenv("TIK_XTWS")) L.xtwson = (atoi(w) >> L.index) & 1;
+        if (const char* w = getenv("TIK_XFG")) L.xfgon = (atoi(w) >> L.index) & 1;
         L.xtrash = reinterpret_cast<float*>(md->trash.p);
     }
     if (const char* e = getenv("TIK_SPLIT")) md->split = e[0] != '0';
@@ -667,7 +691,18 @@ int model_reserve_ws(tik_model* m, Workspace& w, int N, int T) {
         amax = std::max(amax, (size_t)N * t * V * L.cout);
     }
     if (use_xblk(m)) zmax = std::max(zmax, (size_t)N * T * V * XB0_P3_FLOATS);
+    // the second z buffer: the next block's z made inside a fused xtws launch
+    size_t z2max = 0;
+    t = T;
+    for (size_t l = 0; l + 1 < m->layers.size(); ++l) {
+        const Layer& L = m->layers[l];
+        t = Layer::tout(t, L.stride);
+        if (L.index > 0 && L.stride == 1 && L.fuses_gcn_of(m->layers[l + 1])) z2max = std::max(z2max, (size_t)N * t * V * m->layers[l + 1].cout);
+    }
+    t = T;
+    for (const Layer& L : m->layers) t = Layer::tout(t, L.stride);
     int rc;
+    if (z2max && (rc = w.z2.reserve(z2max))) return rc;
     // split-K partials: ksplit * tiles <= 256 + 128 launches of <= 128x128 tiles
     // (cgemm), or up to 8 K slices of the xgemm head's hidden rows
     if ((rc = w.xb.reserve((size_t)N * T * V * 4)) || (rc = w.z.reserve(zmax)) ||
@@ -717,8 +752,11 @@ int tik_model_reserve(tik_model_t m, int N, int T) {
 struct WsPtrs {
     float *xb, *z, *a0, *a1, *hid, *part;
     int ncu;   // persistent grids: the CUs this part runs on
+    float* z2;   // the second z buffer of fused xtws launches (null: none reserved)
 };
-static WsPtrs ptrs_of(const Workspace& w, int ncu) { return WsPtrs{w.xb.p, w.z.p, w.a0.p, w.a1.p, w.hid.p, w.part.p, ncu}; }
+static WsPtrs ptrs_of(const Workspace& w, int ncu) {
+    return WsPtrs{w.xb.p, w.z.p, w.a0.p, w.a1.p, w.hid.p, w.part.p, ncu, w.z2.n ? w.z2.p : nullptr};
+}
 // the workspaces and aux streams of the parts 1 .. np-1 of a split batch
 static int reserve_parts(tik_model* m, int np, int N, int T) {
     int rc;
@@ -859,12 +897,26 @@ static int backbone_x(tik_model_t m, const float* x, int N, int T, float** feat_
         if ((rc = blocks01_x(m, x, N, T, w.a1, st, w))) return rc;
         cur = w.a1; ld = 64;
     }
-    for (const Layer& L : m->layers) {
+    // zin: the current block's z when the previous launch made it (xtws FG); the z
+    // buffers alternate (w.z, w.z2), since a fused launch reads z(l) halo rows of
+    // neighbouring tiles while it writes z(l+1)
+    const float* zin = nullptr;
+    float* zbuf[2] = {w.z, w.z2};
+    int zw = 0;
+    const int nl = (int)m->layers.size();
+    for (int l = 0; l < nl; ++l) {
+        const Layer& L = m->layers[l];
         if (xblk && L.index < 2) continue;
         float* o = bufs[which];
-        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, w.z, o, st, w.ncu, x, m->bn_sc.p, m->bn_sh.p, w.xb);
-        else rc = L.forward_x(cur, ld, N, t, w.z, o, st, w.ncu);
+        const Layer* gn = nullptr;
+        if (l + 1 < nl && w.z2 && L.index > 0 && L.xtws_path(false, ld, t) && L.fuses_gcn_of(m->layers[l + 1])) gn = &m->layers[l + 1];
+        float* zc = zin ? const_cast<float*>(zin) : zbuf[zw];
+        float* zn = zbuf[zc == zbuf[0] ? 1 : 0];
+        if (L.index == 0) rc = L.forward_x(nullptr, 0, N, t, zc, o, st, w.ncu, x, m->bn_sc.p, m->bn_sh.p, w.xb);
+        else rc = L.forward_x(cur, ld, N, t, zc, o, st, w.ncu, nullptr, nullptr, nullptr, nullptr, zin, gn, zn);
         if (rc) return rc;
+        zin = gn ? zn : nullptr;
+        zw = zc == zbuf[0] ? 0 : 1;
         cur = o; ld = L.cout; t = Layer::tout(t, L.stride); which ^= 1;
     }
     *feat_out = const_cast<float*>(cur);

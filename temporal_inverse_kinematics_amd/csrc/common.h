@@ -200,6 +200,7 @@ inline int precision_from_env(int& prec) {
 // reallocate or overwrite memory a captured stream graph points at.
 struct Workspace {
     DevBuf xb, z, a0, a1, hid;       // layer-0 residual input, z, activation ping-pong, head hidden
+    DevBuf z2;                       // the second z of fused launches (xtws FG: block l+1's z beside block l's)
     DevBuf part;                     // split-K partial sums (small-batch launches)
 };
 

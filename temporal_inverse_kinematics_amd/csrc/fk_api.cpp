@@ -9,10 +9,10 @@
 //   fk_landmarks        21 vertex joints + 51 face landmarks + 17 dynamic contour landmarks
 // bf16x3 (default): the blend shapes on xgemm.hip, the skinning on the sparse
 // weights (fk.hip, at most 16 live joints per vertex, fp32 FMAs). Batches of
-// more than one chunk (1024 bodies) run blend + skin per chunk, the chunks
+// more than one chunk (2048 bodies) run blend + skin per chunk, the chunks
 // alternating between the caller's stream and a handle-owned one, so one
 // chunk's HBM-bound skinning runs beside the next chunk's MFMA-bound blend
-// shapes and v_posed (one chunk: 129 MB) can stay in the Infinity Cache.
+// shapes (a 2048-body v_posed is 257 MB, about the Infinity Cache).
 // TIK_FK_SKIN=dense: the skinning as a GEMM on the persistent xgemm kernel
 // (EPI_SKIN; also the path for weights with more than 16 live joints per
 // vertex). fp32: both GEMMs on cgemm.hip.
@@ -48,7 +48,10 @@ struct tik_fk {
     DevBuf WT;         // [V][KJ]     (fp32 path)
     DevHBuf xPT;       // bf16x3 tiles of P^T for xgemm.hip (the blend-shape GEMM, unfused paths)
     bool dense = false;   // TIK_FK_SKIN=dense: the skinning GEMM even when the weights are sparse
-    static constexpr int CHUNK = 1024;   // bodies per blend + skin chunk
+    // bodies per blend + skin chunk (TIK_FK_CHUNK at creation; >= B: one blend + one skin, the
+    // round-4 arrangement). Same box, alternating (profiles/r06_fk_ab_chunk.txt): 2048 4.02-4.04M
+    // bodies/s, 1024 3.93-3.95M, one chunk (4096) 3.91-3.95M
+    int chunk = 2048;
     hipStream_t aux = nullptr;           // the second stream of the chunk pipeline
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ~tik_fk() {
@@ -211,6 +214,7 @@ int tik_fk_create(const tik_tensor* tensors, int n_tensors, int flags, tik_fk_t*
         const int nz = nzmax <= 4 ? 4 : nzmax <= 8 ? 8 : nzmax <= 16 ? 16 : 0;
         const char* e = getenv("TIK_FK_SKIN");   // sparse (default) | dense
         fk->dense = e && !strcmp(e, "dense");
+        if (const char* c = getenv("TIK_FK_CHUNK")) fk->chunk = std::max(1, atoi(c));
         if (nz && !fk->dense) {
             std::vector<int> h((size_t)V * nz * 2, 0);
             for (int v = 0; v < V; ++v) {
@@ -278,7 +282,7 @@ int tik_fk_reserve(tik_fk_t fk, int B) {
     if (B <= fk->cap) return TIK_OK;
     int rc;
     if ((rc = fk->feat.reserve((size_t)B * KP)) || (rc = fk->ablk.reserve((size_t)B * 16 * KJ)) ||
-        (rc = fk->vposed.reserve((size_t)B * fk->ldv)) || (rc = fk->dyn_bin.reserve((size_t)B)) ||
+        (rc = fk->vposed.reserve((size_t)std::max(B, 2 * std::min(fk->chunk, B)) * fk->ldv)) || (rc = fk->dyn_bin.reserve((size_t)B)) ||
         (fk->sp_nz && (rc = fk->ajt.reserve((size_t)B * 55 * 12))) ||
         (rc = fk->zero_transl.upload(std::vector<float>((size_t)B * 3, 0.f))) ||
         (!fk->trash.p && (rc = fk->trash.upload(std::vector<unsigned short>(4096, 0)))))
@@ -352,7 +356,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
     };
 
     if (sparse) {
-        const int nch = (B + tik_fk::CHUNK - 1) / tik_fk::CHUNK;
+        const int CH = fk->chunk, nch = (B + CH - 1) / CH;
         if (nch > 1 && !fk->aux) {
             HIP_TRY(hipStreamCreateWithFlags(&fk->aux, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&fk->ev_fork, hipEventDisableTiming));
@@ -363,10 +367,10 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             HIP_TRY(hipStreamWaitEvent(fk->aux, fk->ev_fork, 0));
         }
         for (int k = 0; k < nch; ++k) {
-            const int b0 = k * tik_fk::CHUNK, n = std::min(tik_fk::CHUNK, B - b0);
+            const int b0 = k * CH, n = std::min(CH, B - b0);
             hipStream_t s = (k & 1) ? fk->aux : st;
             // two v_posed chunk buffers, one per stream (reused in stream order)
-            float* vp = fk->vposed.p + (size_t)(nch > 1 ? (k & 1) * tik_fk::CHUNK : 0) * fk->ldv;
+            float* vp = fk->vposed.p + (size_t)(nch > 1 ? (k & 1) * CH : 0) * fk->ldv;
             if ((rc = blend(b0, n, vp, s)) || (rc = skin(b0, n, vp, s))) return rc;
         }
         if (nch > 1) {

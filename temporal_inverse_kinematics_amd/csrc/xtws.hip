@@ -52,11 +52,15 @@ constexpr int NB = 9;                         // pixel blocks per tile
 constexpr int NKB = 4;                        // 32-channel K blocks
 constexpr int SLOTS = NB * 16 * 512;          // identity / output staging: 144 pixels x 128 channels (73,728)
 // NW waves, each 16 CB = 128 / NW output channels; per-wave slot 144 x 64 CB B (+ 64: slots 16 banks apart)
-template <int NW>
+// FG (the fused next-block gcn): + bias2 [17][128] of block l + 1 staged in LDS
+template <int NW, bool FG>
 struct Cfg {
     static constexpr int CB = 8 / NW, NT = 64 * NW, NLD = (NU + NT - 1) / NT;
     static constexpr int IDW = SLOTS / NW + 64;
-    static constexpr int SMEM = 2 * IMG + NW * IDW;
+    static constexpr int B2 = FG ? V * 128 * 4 + 320 * 4 : 0;   // + A_eff [17][17] (padded to 320)
+    static constexpr int SMEM = 2 * IMG + NW * IDW + B2;
+    static constexpr int NGU = F * V * 8;                 // the gcn split's 16-B fp32 units per K block (1088)
+    static constexpr int NLG = (NGU + NT - 1) / NT;       // ... per thread (3, the last partial)
     static_assert(SMEM <= 160 * 1024, "LDS");
 };
 }  // namespace xw
@@ -85,16 +89,20 @@ typedef __bf16 xwbf16x4 __attribute__((ext_vector_type(4)));
 #define XW_XPF 1   // operand read-ahead (items; 2 spills at 8 waves)
 #endif
 
+#ifndef XW_MIXW
+#define XW_MIXW 7   // FG mix: waves 0-3 make joints 0 .. XW_MIXW - 1, waves 4-7 the rest (7: 55 vs 52 hop<=2 terms)
+#endif
+
 #ifdef TIK_XTUNE
 #define XW_OFF(bit) (a.tune & (bit))
 #else
 #define XW_OFF(bit) false
 #endif
 
-template <int D, int NW>
+template <int D, int NW, bool FG>
 __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
     using namespace xw;
-    using C = Cfg<NW>;
+    using C = Cfg<NW, FG>;
     constexpr int CB = C::CB, NT = C::NT, NLD = C::NLD, IDW = C::IDW;
     __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
     auto pimg = [&](int s) __attribute__((always_inline)) { return smem + (s & 1) * IMG; };
@@ -121,6 +129,20 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         row0 = (w * T + f0) * V;
     };
 
+#ifdef TIK_XTRACE
+    const bool tr = FG && a.trace != nullptr && (wave == 0 || wave == 4);
+#else
+    constexpr bool tr = false;
+#endif
+    // FG phases: 0 T K blocks, 1 T epilogue + out stores, 2 gcn split 0, 3-6 gcn K blocks, 7 y + mix
+    unsigned long long ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if (tr) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (i >= 0) ph_[i] += t - tlast;
+            tlast = t;
+        }
+    };
     const i32x4 rZ = buf_rsrc(a.z, (unsigned)((long long)a.M * a.ldz * 4));
     const i32x4 rXI = buf_rsrc(a.x, (unsigned)((long long)a.M * a.ldx * 4));
     // ---- the halo rows of global step s (tile t_begin + s / 4, K block s % 4) into registers.
@@ -143,27 +165,43 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         for (int i = 0; i < NLD; ++i) load_unit(s, r, i);
     };
     // ---- split registers r (step s) into planes image (s & 1)
-    auto split_unit = [&](int s, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
-        unsigned char* P = pimg(s);
-        const int U = NT * i + tid;
-        if (i + 1 < NLD || U < NU) {
-            const int m = U >> 3, u = U & 7;
-            const int h = m / V, jj = m - h * V;
-            xwbf16x4 p0, p1, p2;
+    // halo unit U (row m = U / 8: frame m / 17, joint m % 17; channels 4 (U % 8) ..) of x -> planes image P
+    auto split_store = [&](unsigned char* P, int U, const f32x4 x) __attribute__((always_inline)) {
+        const int m = U >> 3, u = U & 7;
+        const int h = m / V, jj = m - h * V;
+        xwbf16x4 p0, p1, p2;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
-                const float x = r[i][e];
-                const __bf16 b0 = (__bf16)x;
-                const float r1 = x - (float)b0;
-                const __bf16 b1 = (__bf16)r1;
-                p0[e] = b0;
-                p1[e] = b1;
-                p2[e] = (__bf16)(r1 - (float)b1);
-            }
-            const int hb = (u & 1) * 8;
-            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 0, u >> 1) + hb) = p0;
-            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 1, u >> 1) + hb) = p1;
-            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 2, u >> 1) + hb) = p2;
+        for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
+            const __bf16 b0 = (__bf16)x[e];
+            const float r1 = x[e] - (float)b0;
+            const __bf16 b1 = (__bf16)r1;
+            p0[e] = b0;
+            p1[e] = b1;
+            p2[e] = (__bf16)(r1 - (float)b1);
+        }
+        const int hb = (u & 1) * 8;
+        *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 0, u >> 1) + hb) = p0;
+        *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 1, u >> 1) + hb) = p1;
+        *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 2, u >> 1) + hb) = p2;
+    };
+    auto split_unit = [&](int s, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
+        const int U = NT * i + tid;
+        if (i + 1 < NLD || U < NU) split_store(pimg(s), U, r[i]);
+    };
+    // FG: the halo rows of global step s as raw fp32 units (unit U at byte 16 U) into LDS at dst
+    // by LDS-DMA: instruction k of wave w fills units 64 (NW k + w) + lane (every wave issues
+    // the same count: out-of-range units read zeros into the dead tail)
+    auto dma_halo = [&](int s, unsigned char* dst) __attribute__((always_inline)) {
+        const int t = t_begin + s / NKB, kb = s - (s / NKB) * NKB;
+        int row0, f0;
+        tile_geo(t, row0, f0);
+        const bool live = s < total;
+#pragma unroll
+        for (int k = 0; k < (NU + NT - 1) / NT; ++k) {
+            const int U = 64 * (NW * k + wave) + lane, m = U >> 3, u = U & 7;
+            const int fh = f0 - 1 + m / V;
+            const bool ok = live && U < NU && fh >= 0 && fh < T;
+            dma16(rZ, dst + 1024 * (NW * k + wave), ok ? (unsigned)((long long)(row0 - V + m) * a.ldz * 4 + kb * 128 + u * 16) : DMA_OOB, 0);
         }
     };
     auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
@@ -201,6 +239,10 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
     f32x4 bv[CB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) bv[cb] = *reinterpret_cast<const f32x4*>(a.bias + 16 * (CB * wave + cb) + 4 * g);
+    // FG: block l + 1's bias2 [17][128] and A_eff in LDS (read by the mix, after many barriers)
+    float* const b2s = reinterpret_cast<float*>(smem + 2 * IMG + NW * IDW);
+    if constexpr (FG)
+        for (int i = tid; i < V * 128 + 320; i += NT) b2s[i] = i < V * 128 ? a.bias2[i] : (i - V * 128 < V * V ? a.amix[i - V * 128] : 0.f);
 
     // prologue: step 0 -> planes[0]; steps 1 .. D into registers
     load(0, rb[0]);
@@ -214,6 +256,197 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) acc[j][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // ---- FG: block l + 1's gcn (1x1 conv 128 -> 128 + graph mix + bias2 + ReLU,
+    // st_gcn_aaai18.py:211, gconv_origin.py:56-65) on the tile's output rows, which the
+    // epilogue left in the slots (fp32, this wave's 16 channels per slot, pixel-major).
+    // Per 32-channel K block kb the rows are split once, cooperatively, into planes
+    // image kb & 1 at the rows of halo frame f + 1 (where the T phase's tap 1 reads
+    // them: the same operand reads), this wave's 16 output channels take 9 items x 6
+    // products (weights from L2, two K blocks ahead), and the next K block's split runs
+    // beside them. y then goes through the slots, and the mix runs per (frame, 4
+    // channels) over compile-time joint halves. Products, K order and mix order are
+    // xgraph.hip's: zout equals launch_xgraph's output from `out` bit for bit.
+    xbf16x8 wga[3];
+    auto load_wg = [&](int kb, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
+        // the base through an opaque register: loop-invariant loads would be hoisted out of
+        // the tile loop and their 48 registers held across the T phase
+        const unsigned short* wgp = a.wg;
+        asm volatile("" : "+s"(wgp));
+        if constexpr (FG)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                d[p] = *reinterpret_cast<const xbf16x8*>(wgp + ((((size_t)wave * NKB + kb) * 3 + p) * 64 + lane) * 8);
+    };
+    auto gsplit_unit = [&](int kb, int i) __attribute__((always_inline)) {
+        const int U = NT * i + tid;
+        if ((i + 1 < C::NLG || U < C::NGU) && !XW_OFF(32)) {
+            const int m = U >> 3, u = U & 7;
+            const int f = m / V, jj = m - f * V;
+            const int pix = 16 * (jj >> 1) + 8 * (jj & 1) + f;
+            const f32x4 x = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + (2 * kb + (u >> 2)) * IDW + pix * 64 + (u & 3) * 16);
+            xwbf16x4 p0, p1, p2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
+                const __bf16 b0 = (__bf16)x[e];
+                const float r1 = x[e] - (float)b0;
+                const __bf16 b1 = (__bf16)r1;
+                p0[e] = b0;
+                p1[e] = b1;
+                p2[e] = (__bf16)(r1 - (float)b1);
+            }
+            unsigned char* P = pimg(kb);
+            const int hb = (u & 1) * 8;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, f + 1, 0, u >> 1) + hb) = p0;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, f + 1, 1, u >> 1) + hb) = p1;
+            *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, f + 1, 2, u >> 1) + hb) = p2;
+        }
+    };
+    // K block kb's MFMAs (image kb & 1, weights wk); beside(j) runs after item j
+    auto gmma = [&](int kb, const xbf16x8 (&wk)[3], auto&& beside) __attribute__((always_inline)) {
+        asm volatile("" : "+v"(tid), "+v"(lane));
+        const int g = lane >> 4, px = lane & 15, jb = px >> 3, fb = px & 7;
+        const unsigned char* P = pimg(kb);
+        constexpr int XPF = XW_XPF;
+        xbf16x8 xr[XPF + 1][3];
+        auto rd = [&](int j, xbf16x8 (&d)[3]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(P + xw_unit(2 * j + jb, fb + 1, p, g));
+        };
+#pragma unroll
+        for (int j = 0; j < XPF; ++j) rd(j, xr[j]);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            if (j + XPF < NB) rd(j + XPF, xr[(j + XPF) % (XPF + 1)]);
+            __builtin_amdgcn_sched_barrier(0);
+            const xbf16x8(&x)[3] = xr[j % (XPF + 1)];
+            if (XW_OFF(16)) {
+                beside(j);
+                continue;
+            }
+            // (w0,x2) (w1,x1) (w2,x0) (w0,x1) (w1,x0) (w0,x0): xgraph's product order
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[2], acc[j][0], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[1], x[1], acc[j][0], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[2], x[0], acc[j][0], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[1], acc[j][0], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[1], x[0], acc[j][0], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[0], acc[j][0], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            beside(j);
+        }
+    };
+    // the split units of one K block spread over the 9 items (after items 1, 4, 7)
+    auto spread = [&](int kb) __attribute__((always_inline)) {
+        return [&, kb](int j) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < C::NLG; ++i)
+                if (j == 3 * i + 1) {
+                    gsplit_unit(kb, i);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        };
+    };
+    // s: the tile's last global T step (its next tile's K blocks are s + 1, s + 2)
+    auto gcn_phase = [&](int s, int row0) __attribute__((always_inline)) {
+        // the gcn K blocks carry nothing of the next tile (with the T weights resident the
+        // register file is full): one weight register set, K block kb + 1's load issued
+        // right after K block kb's MFMAs, its latency under the barrier and the split
+        stamp(1);
+        asm volatile("" : "+v"(tid), "+v"(lane));   // lane-derived addresses made here, not hoisted out of the tile loop
+        load_wg(0, wga);
+#pragma unroll
+        for (int i = 0; i < C::NLG; ++i) gsplit_unit(0, i);
+        lds_barrier();   // K block 0's planes landed
+        stamp(2);
+        gmma(0, wga, spread(1));
+        load_wg(1, wga);
+        lds_barrier();
+        stamp(3);
+        gmma(1, wga, spread(2));
+        load_wg(2, wga);
+        lds_barrier();
+        stamp(4);
+        gmma(2, wga, spread(3));
+        load_wg(3, wga);
+        lds_barrier();   // every image read of K block 2 done, the slots' out rows all split
+        stamp(5);
+        gmma(3, wga, [&](int) __attribute__((always_inline)) {});
+        // y through the slots (this wave's 16 channels, pixel-major, as the T epilogue)
+        asm volatile("" : "+v"(tid), "+v"(lane));
+        {
+            const int g = lane >> 4, px = lane & 15;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                *reinterpret_cast<f32x4*>(idw + (16 * j + px) * 64 + g * 16) = acc[j][0];
+                acc[j][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        lds_barrier();   // y complete; every image read done
+        stamp(6);
+        // the next tile's K block 0 as raw fp32 rows into image 1 by LDS-DMA (no registers:
+        // with the T weights resident the mix has none to spare); HBM latency under the mix
+        dma_halo(s + 1, pimg(1));
+        // the mix: thread (frame f, channels 4 c4 ..), waves 0-3 joints 0 .. XW_MIXW - 1, 4-7 the
+        // rest (the COCO hop <= 2 terms split about evenly: 55 / 52 at 7)
+        asm volatile("" : "+v"(tid), "+v"(lane));
+        const int it = tid & 255, f = it >> 5, c4 = it & 31;
+        // A_eff across the wave from LDS (5 VGPRs, v_readlane as xgraph.hip)
+        float amv[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) amv[k] = b2s[V * 128 + 64 * k + lane];
+        auto mix = [&](auto W0c, auto W1c, auto sparse) __attribute__((always_inline)) {
+            constexpr int W0 = decltype(W0c)::value, W1 = decltype(W1c)::value;
+            constexpr bool SP = decltype(sparse)::value;
+            // the joints this half reads (all of them for a dense A_eff)
+            unsigned need = 0;
+#pragma unroll
+            for (int wj = W0; wj < W1; ++wj) need |= SP ? coco_hop2_mask3(wj) : 0x1FFFFu;
+            f32x4 y[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if ((need >> v) & 1u)
+                    y[v] = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + (c4 >> 2) * IDW + (16 * (v >> 1) + 8 * (v & 1) + f) * 64 + (c4 & 3) * 16);
+#pragma unroll
+            for (int wj = W0; wj < W1; ++wj) {
+                f32x4 z = *reinterpret_cast<const f32x4*>(b2s + wj * 128 + 4 * c4);
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    if (!SP || ((coco_hop2_mask3(wj) >> v) & 1u)) {
+                        const float av = __builtin_bit_cast(
+                            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, amv[(v * V + wj) / 64]), (v * V + wj) % 64));
+                        z += av * y[v];
+                    }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) z[e] = z[e] > 0.f ? z[e] : 0.f;
+                xst4(a.zout + (size_t)(row0 + f * V + wj) * a.ldzo + 4 * c4, z, a.nts);
+            }
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I9 = std::integral_constant<int, XW_MIXW>;
+        using I17 = std::integral_constant<int, 17>;
+        if (XW_OFF(64)) {
+        } else if (wave >= NW / 2) {
+            if (a.mix_sparse) mix(I9{}, I17{}, std::true_type{});
+            else mix(I9{}, I17{}, std::false_type{});
+        } else {
+            if (a.mix_sparse) mix(I0{}, I9{}, std::true_type{});
+            else mix(I0{}, I9{}, std::false_type{});
+        }
+        // the next tile's K block 1 into rb (split late in its K block 0); then its K block 0:
+        // raw rows (image 1) -> planes image 0 (every wave's reads of image 0 ended before the
+        // y barrier; the next tile's K block 0 barrier publishes it). This wave's DMA is older
+        // than its z stores (>= min(XW_MIXW, 17 - XW_MIXW)) and those rb loads (NLD)
+        load(s + 2, rb[0]);
+        wait_vm<NLD + (XW_MIXW < V - XW_MIXW ? XW_MIXW : V - XW_MIXW)>();
+        lds_barrier();
+        asm volatile("" : "+v"(tid), "+v"(lane));
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) {
+            const int U = NT * i + tid;
+            if (i + 1 < NLD || U < NU) split_store(pimg(0), U, *reinterpret_cast<const f32x4*>(pimg(1) + U * 16));
+        }
+        stamp(7);
+    };
+
     // one K block; KB compile-time so the weights and the prefetch registers are statically indexed
     auto step = [&](int s, int t, auto KBc) __attribute__((always_inline)) {
         constexpr int kb = decltype(KBc)::value;
@@ -223,7 +456,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
 #if XW_EPIBAR
         // at a tile's first K block the previous tile's epilogue barrier (after this image's
         // split and the last reads of the other one) already holds, except at the run's start
-        if (kb != 0 || t == t_begin) lds_barrier();
+        if (kb != 0 || t == t_begin || FG) lds_barrier();
         constexpr int KDMA = 1;
 #else
         lds_barrier();
@@ -271,21 +504,30 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         // MFMA items (waves leave the barrier together: a split in one piece would
         // idle the MFMA pipe), each unit's register slot reloaded right after (past
         // the run: zeros, never read)
+        // FG: the next tile's K blocks 0 and 1 are split / loaded in the gcn phase (its
+        // planes images are busy until then): K block 2 splits block 3 only, 3 nothing
+        constexpr bool SPL = !FG || kb < NKB - 1, LDN = !FG || kb < NKB - 2;
 #pragma unroll
         for (int n = 0; n < NI; ++n) {
             mfma_n(n);
 #pragma unroll
             for (int i = 0; i < NLD; ++i)
-                if (n == (XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD))) {
+                // FG K block 0: its rb was loaded just before the tile, so its split units go late
+                if (SPL && n == (FG && kb == 0 ? NI / 2 + (i * NI) / (2 * NLD) : XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD))) {
                     if (!XW_OFF(2)) split_unit(s + 1, rb[nb], i);
-                    load_unit(s + 1 + D, rb[nb], i);
+                    if (LDN) load_unit(s + 1 + D, rb[nb], i);
                     __builtin_amdgcn_sched_barrier(0);
                 }
         }
         if constexpr (kb == NKB - 1) {
             // ---- epilogue: (acc + x) + bias, ReLU. The identity DMA of this tile was issued
             // before the register loads of its K blocks KDMA .. 3: at most that many may stay in flight
-            wait_vm<(NKB - KDMA) * NLD>();
+            if constexpr (FG) {
+                stamp(0);
+                wait_vm<0>();   // the identity DMA landed (the K-block loads since were consumed)
+            } else {
+                wait_vm<(NKB - KDMA) * NLD>();
+            }
 #pragma unroll
             for (int j = 0; j < NB; ++j)
 #pragma unroll
@@ -317,14 +559,37 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
     // to their older SIMD partners on every segment: MI355X_MICROARCH.md, two waves per SIMD):
     // 0.265 vs 0.272 ms on L3. 8 waves only (the condition must be wave-uniform: readfirstlane)
     if (NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-    for (int t = t_begin; t < t_end; ++t) {
+    stamp(-1);
+    auto tphase = [&](int t) __attribute__((always_inline)) {
         const int s0 = (t - t_begin) * NKB;
         step(s0, t, std::integral_constant<int, 0>{});
         step(s0 + 1, t, std::integral_constant<int, 1>{});
         step(s0 + 2, t, std::integral_constant<int, 2>{});
         step(s0 + 3, t, std::integral_constant<int, 3>{});
+    };
+    if constexpr (FG) {
+        // the loop body is [gcn phase of tile t, T phase of tile t + 1]: the registers the gcn
+        // phase loads for the next tile are used in the same iteration, so the loop header (a
+        // control-flow merge) does not wait for them, or for every store, with vmcnt(0)
+        tphase(t_begin);
+        for (int t = t_begin; t < t_end; ++t) {
+            int row0, f0;
+            tile_geo(t, row0, f0);
+            gcn_phase((t - t_begin) * NKB + NKB - 1, row0);
+            if (t + 1 < t_end) tphase(t + 1);
+        }
+    } else {
+        for (int t = t_begin; t < t_end; ++t) tphase(t);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef TIK_XTRACE
+    if (tr && lane == 0) {
+        unsigned long long* o = a.trace + 16 * (size_t)blockIdx.x + (wave == 4 ? 8 : 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = ph_[i];
+        if (wave == 0) o[7] |= (unsigned long long)(t_end - t_begin) << 48;
+    }
+#endif
 }
 
 bool xtws_ok(const XTConvArgs& a) {
@@ -336,8 +601,9 @@ hipError_t launch_xtws(const XTConvArgs& a, int ncu, hipStream_t st) {
     if (a.M <= 0) return hipSuccess;
     if (!xtws_ok(a) || !a.z || !a.x || !a.wp || !a.bias || !a.out || !a.trash || ncu <= 0 || a.M % (17 * a.T) != 0)
         return hipErrorInvalidValue;
+    if (a.wg && (!a.bias2 || !a.amix || !a.zout || a.ldzo % 4 || a.ldzo < 128 || a.zout == a.z)) return hipErrorInvalidValue;
     // the buffer offsets are 32-bit: launches of whole windows, < 2 GiB of conv input and identity rows each
-    const long long win = 17LL * a.T, win_bytes = win * std::max(a.ldz, a.ldx) * 4;
+    const long long win = 17LL * a.T, win_bytes = win * std::max(std::max(a.ldz, a.ldx), a.wg ? a.ldzo : 0) * 4;
     if (win_bytes >= (1LL << 31)) return hipErrorInvalidValue;
     const long long wper = std::max(1LL, ((1LL << 31) - 1) / win_bytes);
     const long long rows_per = wper * win;
@@ -348,10 +614,12 @@ hipError_t launch_xtws(const XTConvArgs& a, int ncu, hipStream_t st) {
         c.z = a.z + (size_t)r0 * a.ldz;
         c.x = a.x + (size_t)r0 * a.ldx;
         c.out = a.out + (size_t)r0 * a.ldo;
+        if (a.wg) c.zout = a.zout + (size_t)r0 * a.ldzo;
         const int ntiles = (int)(c.M / win) * (a.T / xw::F);
         // 8 waves (two per SIMD, 16 channels each); 4 waves of 32 channels (one per SIMD, the weights
         // through AGPRs: v_accvgpr_read before every MFMA group) measured 0.364 vs 0.288 ms
-        hipLaunchKernelGGL((xtws_kernel<XW_D, 8>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
+        if (a.wg) hipLaunchKernelGGL((xtws_kernel<XW_D, 8, true>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
+        else hipLaunchKernelGGL((xtws_kernel<XW_D, 8, false>), dim3(std::min(ntiles, ncu)), dim3(512), 0, st, c);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -456,6 +456,39 @@ def test_xtws_vs_tiled_and_oracle(n, T):
     assert np.abs(a[idx].cpu().numpy() - ref).max() < TOL
 
 
+@pytest.mark.parametrize("n,T", [(1024, 64), (3, 16), (5, 48), (2, 9), (1, 16), (7, 128), (257, 32), (33, 96), (37, 64)])
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_xtws_fused_gcn_vs_layered(n, T, split):
+    """the next block's spatial half (gcn 1x1 conv + graph
+    mix + BN + ReLU, st_gcn_aaai18.py:211 of block l + 1) inside block l's
+    temporal-conv launch (xtws.hip FG, the default for L3 -> G4 and L4 -> G5:
+    the tile's output rows go from LDS through block l + 1's gcn, no XGW
+    launch re-reads them from HBM) against separate XTW + XGW launches
+    (TIK_XFG=0). Same products, K order and mix order as xgraph.hip: the
+    poses and features are bitwise equal — at the bench size, one / three /
+    eight tiles per window, T=9 (L3 has 5 frames: no xtws, no fusion), a
+    single tile, uneven tile counts per workgroup; one stream and the
+    two-part split (the second z buffer per part)."""
+    from temporal_inverse_kinematics_amd import synthetic as syn
+    fu = _model_with_env("bf16x3", TIK_SPLIT=split)
+    ly = _model_with_env("bf16x3", TIK_SPLIT=split, TIK_XFG=0)
+    xh = syn.synthetic_windows(n, T, seed=n * 11 + T)
+    x = torch.from_numpy(xh).cuda()
+    with torch.no_grad():
+        a = fu(x)["poses"].clone()
+        b = ly(x)["poses"]
+        fa = fu.backbone_features(x)
+        fb = ly.backbone_features(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(fa, fb), float((fa - fb).abs().max())
+    assert torch.equal(a, b), float((a - b).abs().max())
+    sd = {k: v.detach().cpu().numpy() for k, v in fu.state_dict().items()}
+    idx = [0, n - 1]
+    ref = orc.pose_regressor(xh[idx], sd)["poses"]
+    assert np.abs(a[idx].cpu().numpy() - ref).max() < TOL
+
+
 def test_run_test_end_to_end_and_cli(tmp_path):
     """inference.run_test (`/root/reference/inference.py:110-145`) end to end on
     the reference's shipped moveai sample (data/sample_3d_poses/

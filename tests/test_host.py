@@ -163,6 +163,6 @@ def test_bench_kernel_symbols_resolve():
     names = set()
     for p in glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")):
         names |= {k.replace("void ", "").strip() for k in json.load(open(p)).get("kernels", {})}
-    for label in ("XT128", "XH128", "XR", "XGW", "XTW", "XB0", "XB1", "XG128", "XP64", "G0f_raw"):
+    for label in ("XT128", "XH128", "XR", "XGW", "XTWG", "XB0", "XB1", "XG128", "XP64", "G0f_raw"):
         sym = bench.kernel_symbol(label, "bf16x3")
         assert sym and any(n == sym or ("<" not in sym and n.startswith(sym + "<")) for n in names), (label, sym)

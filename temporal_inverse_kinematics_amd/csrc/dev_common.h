@@ -73,6 +73,14 @@ __device__ __forceinline__ void dma16(const i32x4 r, void* dst, unsigned voff, i
     tik_llvm_raw_buffer_load_lds(r, (__attribute__((address_space(3))) unsigned*)dst, 16, (int)voff, soff, 0, TIK_DMA_AUX);
 }
 
+// dma16 as inline asm: invisible to the compiler's vmcnt bookkeeping (no wait before
+// later accesses of the LDS it writes, not counted either); the caller orders every
+// use with an explicit wait_vm (loads, stores and DMAs retire vmcnt in issue order)
+__device__ __forceinline__ void dma16_asm(const i32x4 r, void* dst, unsigned voff) {
+    const unsigned m = (unsigned)(unsigned long long)(__attribute__((address_space(3))) unsigned char*)dst;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r) : "memory", "m0");
+}
+
 constexpr unsigned DMA_OOB = 0x80000000u;
 
 template <int N>

@@ -104,12 +104,16 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
     using namespace xw;
     using C = Cfg<NW, FG>;
     constexpr int CB = C::CB, NT = C::NT, NLD = C::NLD, IDW = C::IDW;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
-    auto pimg = [&](int s) __attribute__((always_inline)) { return smem + (s & 1) * IMG; };
+    constexpr int NHD = (NU + NT - 1) / NT;   // FG: halo DMA instructions per wave
+    // the two planes images and the rest (slots, FG's bias2 + A_eff) as separate LDS objects:
+    // the compiler then knows an LDS-DMA into one image cannot alias reads of the other or of
+    // the slots, and adds no vmcnt(0) before them
+    __shared__ __attribute__((aligned(16))) unsigned char img0[IMG], img1[IMG], sl[C::SMEM - 2 * IMG];
+    auto pimg = [&](int kb) __attribute__((always_inline)) { return (kb & 1) ? img1 : img0; };
 
     int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    unsigned char* const idw = smem + 2 * IMG + wave * IDW;
+    unsigned char* const idw = sl + wave * IDW;
     const int T = a.T, tpw = T / F;
     const int ntiles = a.M / (V * T) * tpw;
     int t_begin, t_end;
@@ -184,24 +188,26 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 1, u >> 1) + hb) = p1;
         *reinterpret_cast<xwbf16x4*>(P + xw_unit(jj, h, 2, u >> 1) + hb) = p2;
     };
-    auto split_unit = [&](int s, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
+    auto split_unit = [&](int kb, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
         const int U = NT * i + tid;
-        if (i + 1 < NLD || U < NU) split_store(pimg(s), U, r[i]);
+        if (i + 1 < NLD || U < NU) split_store(pimg(kb), U, r[i]);
     };
     // FG: the halo rows of global step s as raw fp32 units (unit U at byte 16 U) into LDS at dst
     // by LDS-DMA: instruction k of wave w fills units 64 (NW k + w) + lane (every wave issues
     // the same count: out-of-range units read zeros into the dead tail)
+    // (by inline asm: the compiler does not track these LDS writes, so it adds no vmcnt wait
+    // before later accesses of dst, nor counts them; the caller waits with wait_vm)
     auto dma_halo = [&](int s, unsigned char* dst) __attribute__((always_inline)) {
         const int t = t_begin + s / NKB, kb = s - (s / NKB) * NKB;
         int row0, f0;
         tile_geo(t, row0, f0);
         const bool live = s < total;
 #pragma unroll
-        for (int k = 0; k < (NU + NT - 1) / NT; ++k) {
+        for (int k = 0; k < NHD; ++k) {
             const int U = 64 * (NW * k + wave) + lane, m = U >> 3, u = U & 7;
             const int fh = f0 - 1 + m / V;
             const bool ok = live && U < NU && fh >= 0 && fh < T;
-            dma16(rZ, dst + 1024 * (NW * k + wave), ok ? (unsigned)((long long)(row0 - V + m) * a.ldz * 4 + kb * 128 + u * 16) : DMA_OOB, 0);
+            dma16_asm(rZ, dst + 1024 * (NW * k + wave), ok ? (unsigned)((long long)(row0 - V + m) * a.ldz * 4 + kb * 128 + u * 16) : DMA_OOB);
         }
     };
     auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) bv[cb] = *reinterpret_cast<const f32x4*>(a.bias + 16 * (CB * wave + cb) + 4 * g);
     // FG: block l + 1's bias2 [17][128] and A_eff in LDS (read by the mix, after many barriers)
-    float* const b2s = reinterpret_cast<float*>(smem + 2 * IMG + NW * IDW);
+    float* const b2s = reinterpret_cast<float*>(sl + NW * IDW);
     if constexpr (FG)
         for (int i = tid; i < V * 128 + 320; i += NT) b2s[i] = i < V * 128 ? a.bias2[i] : (i - V * 128 < V * V ? a.amix[i - V * 128] : 0.f);
 
@@ -274,8 +280,17 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         asm volatile("" : "+s"(wgp));
         if constexpr (FG)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
-                d[p] = *reinterpret_cast<const xbf16x8*>(wgp + ((((size_t)wave * NKB + kb) * 3 + p) * 64 + lane) * 8);
+            for (int p = 0; p < 3; ++p) {
+                const auto* q = (const __attribute__((address_space(1))) xbf16x8*)(wgp + ((((size_t)wave * NKB + kb) * 3 + p) * 64 + lane) * 8);
+                if (kb == NKB - 1)
+                    // K block 3's planes by inline asm, waited for explicitly (wait_wg3) with the
+                    // halo DMA issued after them still in flight; the compiler, not seeing that
+                    // DMA, would wait with vmcnt(0)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d[p]) : "v"(q) : "memory");
+                else
+                    // a global (not flat) load: a pending flat load makes every later vmcnt wait a vmcnt(0)
+                    d[p] = *q;
+            }
     };
     auto gsplit_unit = [&](int kb, int i) __attribute__((always_inline)) {
         const int U = NT * i + tid;
@@ -283,7 +298,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             const int m = U >> 3, u = U & 7;
             const int f = m / V, jj = m - f * V;
             const int pix = 16 * (jj >> 1) + 8 * (jj & 1) + f;
-            const f32x4 x = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + (2 * kb + (u >> 2)) * IDW + pix * 64 + (u & 3) * 16);
+            const f32x4 x = *reinterpret_cast<const f32x4*>(sl + (2 * kb + (u >> 2)) * IDW + pix * 64 + (u & 3) * 16);
             xwbf16x4 p0, p1, p2;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
@@ -369,6 +384,13 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         load_wg(3, wga);
         lds_barrier();   // every image read of K block 2 done, the slots' out rows all split
         stamp(5);
+        // the next tile's K block 0 as raw fp32 rows by LDS-DMA into image 0, free since K block
+        // 2's reads (no registers: with the T weights resident the mix has none to spare); HBM
+        // latency under K block 3's MFMAs and the mix
+        dma_halo(s + 1, pimg(0));
+        // K block 3's weights landed: only the halo DMA (NHD instructions per wave) is younger
+        static_assert(NHD == 3, "wait_wg3");
+        asm volatile("s_waitcnt vmcnt(3)" : "+v"(wga[0]), "+v"(wga[1]), "+v"(wga[2]));
         gmma(3, wga, [&](int) __attribute__((always_inline)) {});
         // y through the slots (this wave's 16 channels, pixel-major, as the T epilogue)
         asm volatile("" : "+v"(tid), "+v"(lane));
@@ -382,9 +404,6 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         }
         lds_barrier();   // y complete; every image read done
         stamp(6);
-        // the next tile's K block 0 as raw fp32 rows into image 1 by LDS-DMA (no registers:
-        // with the T weights resident the mix has none to spare); HBM latency under the mix
-        dma_halo(s + 1, pimg(1));
         // the mix: thread (frame f, channels 4 c4 ..), waves 0-3 joints 0 .. XW_MIXW - 1, 4-7 the
         // rest (the COCO hop <= 2 terms split about evenly: 55 / 52 at 7)
         asm volatile("" : "+v"(tid), "+v"(lane));
@@ -404,7 +423,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
 #pragma unroll
             for (int v = 0; v < V; ++v)
                 if ((need >> v) & 1u)
-                    y[v] = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + (c4 >> 2) * IDW + (16 * (v >> 1) + 8 * (v & 1) + f) * 64 + (c4 & 3) * 16);
+                    y[v] = *reinterpret_cast<const f32x4*>(sl + (c4 >> 2) * IDW + (16 * (v >> 1) + 8 * (v & 1) + f) * 64 + (c4 & 3) * 16);
 #pragma unroll
             for (int wj = W0; wj < W1; ++wj) {
                 f32x4 z = *reinterpret_cast<const f32x4*>(b2s + wj * 128 + 4 * c4);
@@ -431,18 +450,23 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             if (a.mix_sparse) mix(I0{}, I9{}, std::true_type{});
             else mix(I0{}, I9{}, std::false_type{});
         }
-        // the next tile's K block 1 into rb (split late in its K block 0); then its K block 0:
-        // raw rows (image 1) -> planes image 0 (every wave's reads of image 0 ended before the
-        // y barrier; the next tile's K block 0 barrier publishes it). This wave's DMA is older
-        // than its z stores (>= min(XW_MIXW, 17 - XW_MIXW)) and those rb loads (NLD)
+        // the next tile's K block 1 into rb (split late in its K block 0); then its K block 0,
+        // in place: every thread reads its raw units of image 0, a barrier, then writes their
+        // planes into image 0 (the next tile's K block 0 barrier publishes them). This wave's
+        // DMA is older than its z stores (>= min(XW_MIXW, 17 - XW_MIXW)) and those rb loads (NLD)
         load(s + 2, rb[0]);
         wait_vm<NLD + (XW_MIXW < V - XW_MIXW ? XW_MIXW : V - XW_MIXW)>();
         lds_barrier();
         asm volatile("" : "+v"(tid), "+v"(lane));
+        // (units past NU read inside image 0 and are not used)
+        f32x4 raw[NLD];
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) raw[i] = *reinterpret_cast<const f32x4*>(pimg(0) + (NT * i + tid) * 16);
+        lds_barrier();   // every raw unit read (lgkmcnt(0)) before any plane overwrites it
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int U = NT * i + tid;
-            if (i + 1 < NLD || U < NU) split_store(pimg(0), U, *reinterpret_cast<const f32x4*>(pimg(1) + U * 16));
+            if (i + 1 < NLD || U < NU) split_store(pimg(0), U, raw[i]);
         }
         stamp(7);
     };
@@ -469,7 +493,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             dma_ident(t);
             __builtin_amdgcn_sched_barrier(0);
         }
-        const unsigned char* P = pimg(s);
+        const unsigned char* P = pimg(kb);   // s & 1 == kb & 1 (4 K blocks per tile)
         const int jb = px >> 3, fb = px & 7;
         // operand ring over the 27 (block, tap) items: item n + XPF's planes are read while item n's MFMAs run
         constexpr int NI = NB * 3, XPF = XW_XPF;
@@ -514,7 +538,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
             for (int i = 0; i < NLD; ++i)
                 // FG K block 0: its rb was loaded just before the tile, so its split units go late
                 if (SPL && n == (FG && kb == 0 ? NI / 2 + (i * NI) / (2 * NLD) : XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD))) {
-                    if (!XW_OFF(2)) split_unit(s + 1, rb[nb], i);
+                    if (!XW_OFF(2)) split_unit(kb + 1, rb[nb], i);
                     if (LDN) load_unit(s + 1 + D, rb[nb], i);
                     __builtin_amdgcn_sched_barrier(0);
                 }
@@ -549,7 +573,7 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
                 const int q = tid + NT * i, pix = q >> 5, cu = q & 31;
                 const int j = pix >> 4, pp = pix & 15, jj = 2 * j + (pp >> 3);
                 const int ws = cu / (4 * CB), pc = cu - ws * (4 * CB);
-                const f32x4 v = *reinterpret_cast<const f32x4*>(smem + 2 * IMG + ws * IDW + pix * (64 * CB) + pc * 16);
+                const f32x4 v = *reinterpret_cast<const f32x4*>(sl + ws * IDW + pix * (64 * CB) + pc * 16);
                 float* o = jj < V ? a.out + (size_t)(row0 + (pp & 7) * V + jj) * a.ldo + cu * 4 : a.trash + (tid & 255) * 4;
                 if (!XW_OFF(8)) xst4(o, v, a.nts);
             }

@@ -130,17 +130,31 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
 
     // ---- block 1: the x image of a tile (joint-major rows R = 12 j + f, f = input frame q0 - 1 + f)
     const i32x4 rX = buf_rsrc(RAW ? nullptr : (const void*)a.xp3, RAW ? 0u : (unsigned)((long long)QO * V * ROWB));
+    // the tile-invariant part of each DMA lane's source offset, made once: (frame f of
+    // the 12, joint j, plane, swizzled unit) -> byte offset from the tile's first input
+    // frame row | f << 24 | bit 31 = past the image (the per-tile work is then an add
+    // and a range check instead of two divisions per instruction)
+    constexpr int NXI = (XINST + 7) / 8;   // DMA instructions per wave
+    unsigned xpre[NXI];
+#pragma unroll
+    for (int i = 0; i < NXI; ++i) {
+        const int ins = wave + 8 * i;
+        const int U = ins * 64 + lane;
+        const int R = U / 24, k = U - R * 24, plane = k >> 3, up = k & 7;
+        const int j = R / FIN, f = R - j * FIN;
+        xpre[i] = U < XUNITS && ins < XINST ? (unsigned)((f * V + j) * ROWB + plane * 128 + ((up ^ ((R + j) & 7)) << 4)) | ((unsigned)f << 24)
+                                            : 0x80000000u;
+    }
     auto issue_x = [&](int tile) __attribute__((always_inline)) {
         const int q0 = tile * F;
 #pragma unroll
-        for (int i = 0; i < (XINST + 7) / 8; ++i) {
+        for (int i = 0; i < NXI; ++i) {
             const int ins = wave + 8 * i;
             if (ins >= XINST) break;
-            const int U = ins * 64 + lane;           // LDS unit of this lane
-            const int R = U / 24, k = U - R * 24, plane = k >> 3, up = k & 7;
-            const int j = R / FIN, f = R - j * FIN, q = q0 - 1 + f;
-            const bool ok = U < XUNITS && q >= 0 && q < QO;
-            const unsigned off = ok ? (unsigned)(((long long)q * V + j) * ROWB + plane * 128 + ((up ^ ((R + j) & 7)) << 4)) : DMA_OOB;
+            const unsigned c = xpre[i];
+            const int q = q0 - 1 + (int)((c >> 24) & 0x7F);
+            const bool ok = !(c >> 31) && q >= 0 && q < QO;
+            const unsigned off = ok ? (unsigned)((long long)(q0 - 1) * V * ROWB) + (c & 0xFFFFFFu) : DMA_OOB;
             dma16(rX, ximg + ins * 1024, off, 0);
         }
     };

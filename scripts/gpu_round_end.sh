@@ -8,14 +8,18 @@ export TMPDIR=/tmp
 OUT=gpurun_out
 TAG=${1:-r01}
 mkdir -p $OUT
-ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+ok() { local rc=$1; [ "$rc" -eq 0 ]; }
+PHASE=${2:-all}   # tests | measure | all
 echo "== build"; python -m temporal_inverse_kinematics_amd._build > $OUT/build.log 2>&1 || exit 2
+if [ "$PHASE" != measure ]; then
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?
 tail -3 $OUT/pytest_gpu_$TAG.log; echo "pytest rc=$rc"; ok $rc || exit $rc
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1; rc=$?
 tail -2 $OUT/smoke_$TAG.log; echo "smoke rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
+[ "$PHASE" = tests ] && exit 0
 echo "== pmc passes + kernel stats (single-stream)"
 bash scripts/gpu_pmc_all.sh $TAG; rc=$?
 echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc

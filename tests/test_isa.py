@@ -56,3 +56,34 @@ def test_no_lgkmcnt_partial_wait_with_smem_outstanding(src, tmp_path):
     assert res, "no kernels found"
     bad = {k: v[1][:3] for k, v in res.items() if v[1]}
     assert not bad, bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_lds_dma_sets_m0_after_inline_asm_dma(tmp_path):
+    """xtws.hip issues the next tile's halo DMA as inline asm (dev_common.h
+    dma16_asm: `s_mov_b32 m0` + `buffer_load_dwordx4 ... lds`), which the
+    compiler cannot see writing M0 (a reserved register: the clobber is only a
+    warning). Every compiler-emitted LDS-DMA after such a block must therefore
+    write M0 itself before it, never reuse a value set before the asm."""
+    text = _asm("xtws.hip", tmp_path).read_text()
+    lines = text.splitlines()
+    in_asm = stale = False
+    n = 0
+    for ln in lines:
+        t = ln.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if in_asm:
+            if "m0" in t:
+                stale = True
+            continue
+        if re.match(r"s_(mov|add)_[bi]32\s+m0,", t) or t.startswith("s_endpgm"):
+            stale = False
+        if t.startswith("buffer_load_dword") and t.endswith(" lds"):
+            n += 1
+            assert not stale, "compiler LDS-DMA after an inline-asm M0 write without its own M0 set: " + t
+    assert n > 0

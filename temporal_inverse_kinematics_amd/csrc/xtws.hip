@@ -34,6 +34,10 @@
 // distinct 4-bank slots).
 // Products as xgemm (bf16x3, six products per K block), fp32 accumulation in
 // the order (K block, tap), XT128's K order: the two are bitwise equal.
+// FG (xtws_kernel<.., true>, round 6, the default for L3/L4): each tile's output
+// rows, still in the slots, also go through block l + 1's gcn 1x1 conv + graph
+// mix + BN + ReLU (XTWG; see "FG:" below and DESIGN.md §2a), bit for bit what
+// launch_xgraph makes from `out`.
 #include <algorithm>
 #include <type_traits>
 

@@ -308,8 +308,12 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
         // Software pipeline inside the step: the A reads of step k+1 and the
         // first weight block's reads, then per column block j the next block's
         // reads are issued BEFORE the 6 FM MFMAs of j (so no read is waited on
-        // right after its issue), and fragment j's split of step k+1 runs
-        // between block j's MFMAs. sched_barriers keep the blocks in this order.
+        // right after its issue), and a quarter of one fragment's split of step
+        // k+1 runs between block j's MFMAs, one VALU per MFMA (round 6: the whole
+        // split in blocks 0-1, and one step of each unrolled pair had its split
+        // sunk past all its MFMAs to the next step's start, 80 VALU in a row;
+        // spread and pinned, XT128 runs 6-10 % faster). sched_barriers keep the
+        // blocks in this order.
         xbf16x8 bb[2][3];
         __builtin_amdgcn_sched_barrier(0);
 #ifdef TIK_XORDER
@@ -342,16 +346,23 @@ __global__ __launch_bounds__(64 * NW_, NW_ == 8 ? 1 : 2) void xgemm_kernel(XArgs
                 mma(u0[i], b[1], acc[i][j]);
                 mma(u0[i], b[0], acc[i][j]);
             }
-            if (j < FM && !(tune & 8)) xsplit8(alo[j], ahi[j], v0[j], v1[j], v2[j]);
-            // past the last block the remaining fragments' splits
-            if (j == FN - 1)
+            // the next step's split in 4 * FM parts spread evenly over the FN column blocks
+            constexpr int PPJ = (4 * FM + FN - 1) / FN;
 #pragma unroll
-                for (int i = FN; i < FM; ++i) xsplit8(alo[i], ahi[i], v0[i], v1[i], v2[i]);
+            for (int pp = 0; pp < PPJ; ++pp) {
+                const int p = j * PPJ + pp;
+                if (p < 4 * FM && !(tune & 8)) {
+                    xsplit8_part(alo[p >> 2], ahi[p >> 2], v0[p >> 2], v1[p >> 2], v2[p >> 2], p & 3);
+                    // pin the finished fragment here (left alone, the split of one step of a pair
+                    // was sunk past its MFMAs to the next step's start)
+                    if ((p & 3) == 3) asm volatile("" : "+v"(v0[p >> 2]), "+v"(v1[p >> 2]), "+v"(v2[p >> 2]));
+                }
+            }
             if (j + 1 < FN) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
             for (int q = 0; q < 6 * FM; ++q) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }

@@ -25,6 +25,21 @@ __device__ __forceinline__ void xsplit8(const f32x4 lo, const f32x4 hi, xbf16x8&
     }
 }
 
+// part q (0..3) of xsplit8: elements 2q, 2q + 1 (the same arithmetic), so a
+// fragment's split can be spread over four MFMA groups
+__device__ __forceinline__ void xsplit8_part(const f32x4 lo, const f32x4 hi, xbf16x8& p0, xbf16x8& p1, xbf16x8& p2, int q) {
+#pragma unroll
+    for (int e = 2 * q; e < 2 * q + 2; ++e) {
+        const float x = e < 4 ? lo[e] : hi[e - 4];
+        const __bf16 b0 = (__bf16)x;
+        const float r1 = x - (float)b0;
+        const __bf16 b1 = (__bf16)r1;
+        p0[e] = b0;
+        p1[e] = b1;
+        p2[e] = (__bf16)(r1 - (float)b1);
+    }
+}
+
 // epilogue stores of output tiles: nontemporal for the backbone's layer
 // outputs (XArgs::nts; same-box A/B +0.9 % IK frames/s), plain for split-K
 // partials and the FK GEMMs (re-read at once; NT measured slower there)

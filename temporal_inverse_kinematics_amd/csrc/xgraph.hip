@@ -99,44 +99,46 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
     // Every wave issues NLD loads for every step, past the batch / the run as
     // out-of-range (zero) loads: no branch, so the compiler's vmcnt accounting
     // stays exact (at a merge it falls back to the fewest outstanding, i.e. vmcnt(0))
-    auto load = [&](int s, f32x4 (&r)[NLD]) __attribute__((always_inline)) {
+    auto load_unit = [&](int s, f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
         const int t = t_begin + s / NK, kb = s - (s / NK) * NK;
         const int q0 = tile_fg(t) * FR;
         const bool live = s < total;
+        const int U = 512 * i + tid, m = U >> 3, u = U & 7;
+        const int q = q0 + m / V;
+        const unsigned off = live && U < NU && q < QO && !XG_OFF(1) ? (unsigned)(((long long)q0 * V + m) * a.ldx * 4 + kb * 128 + u * 16) : DMA_OOB;
+        r[i] = tik_llvm_raw_buffer_load_v4f32(rX, (int)off, 0, 0);
+    };
+    auto load = [&](int s, f32x4 (&r)[NLD]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < NLD; ++i) {
-            const int U = 512 * i + tid, m = U >> 3, u = U & 7;
-            const int q = q0 + m / V;
-            const unsigned off = live && U < NU && q < QO && !XG_OFF(1) ? (unsigned)(((long long)q0 * V + m) * a.ldx * 4 + kb * 128 + u * 16) : DMA_OOB;
-            r[i] = tik_llvm_raw_buffer_load_v4f32(rX, (int)off, 0, 0);
-        }
+        for (int i = 0; i < NLD; ++i) load_unit(s, r, i);
     };
     // ---- split registers r (this lane's units of step s) into planes image (s & 1)
-    auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
+    auto split_unit = [&](int s, const f32x4 (&r)[NLD], int i) __attribute__((always_inline)) {
         unsigned char* P = pimg(s);
+        const int U = 512 * i + tid;
+        if (i + 1 < NLD || U < NU) {
+            const int m = U >> 3, u = U & 7;
+            const int R = 16 * (m % V) + m / V;
+            xbf16x4 p0, p1, p2;
 #pragma unroll
-        for (int i = 0; i < NLD; ++i) {
-            const int U = 512 * i + tid;
-            if (i + 1 < NLD || U < NU) {
-                const int m = U >> 3, u = U & 7;
-                const int R = 16 * (m % V) + m / V;
-                xbf16x4 p0, p1, p2;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
-                    const float x = r[i][e];
-                    const __bf16 b0 = (__bf16)x;
-                    const float r1 = x - (float)b0;
-                    const __bf16 b1 = (__bf16)r1;
-                    p0[e] = b0;
-                    p1[e] = b1;
-                    p2[e] = (__bf16)(r1 - (float)b1);
-                }
-                const int h = (u & 1) * 8;
-                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 0, u >> 1) + h) = p0;
-                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 1, u >> 1) + h) = p1;
-                *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 2, u >> 1) + h) = p2;
+            for (int e = 0; e < 4; ++e) {   // xsplit8's arithmetic, 4 channels
+                const float x = r[i][e];
+                const __bf16 b0 = (__bf16)x;
+                const float r1 = x - (float)b0;
+                const __bf16 b1 = (__bf16)r1;
+                p0[e] = b0;
+                p1[e] = b1;
+                p2[e] = (__bf16)(r1 - (float)b1);
             }
+            const int h = (u & 1) * 8;
+            *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 0, u >> 1) + h) = p0;
+            *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 1, u >> 1) + h) = p1;
+            *reinterpret_cast<xbf16x4*>(P + xg_unit(R, 2, u >> 1) + h) = p2;
         }
+    };
+    auto split = [&](int s, const f32x4 (&r)[NLD]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NLD; ++i) split_unit(s, r, i);
     };
 
     // weights of this wave's 16 channels for the current pass. Two passes (256
@@ -218,15 +220,38 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         };
 #pragma unroll
         for (int j = 0; j < XPF; ++j) rd(j, xb[j]);
+        if constexpr (NP == 2) {
+            // two-pass (256-channel) layers: the next step's split one unit every third joint
+            // from joint 1 on, each unit's register slot reloaded right after it (past the run:
+            // zeros, never read); the asm keeps the unit's VALU and LDS writes there. XGW.L7
+            // -4 %, L6 -1 %; the HBM-bound one-pass layers are 0.5 % faster with the block below
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_j(j);
-        stamp(1);
-        if (!XG_OFF(2)) split(s + 1, rb[nb]);   // VALU + LDS writes beside the MFMAs (past the run: zeros, never read)
-        stamp(2);
-        load(s + 1 + D, rb[nb]);
-        stamp(3);
+            for (int j = 0; j < V; ++j) {
+                mfma_j(j);
+                if (j % 3 == 1 && j / 3 < NLD) {
+                    const int i = j / 3;
+                    if (!XG_OFF(2)) split_unit(s + 1, rb[nb], i);
+                    load_unit(s + 1 + D, rb[nb], i);
+                    asm volatile("" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (j == 3) {
+                    stamp(1);
+                    stamp(2);
+                    stamp(3);
+                }
+            }
+        } else {
 #pragma unroll
-        for (int j = 4; j < V; ++j) mfma_j(j);
+            for (int j = 0; j < 4; ++j) mfma_j(j);
+            stamp(1);
+            if (!XG_OFF(2)) split(s + 1, rb[nb]);   // VALU + LDS writes beside the MFMAs (past the run: zeros, never read)
+            stamp(2);
+            load(s + 1 + D, rb[nb]);
+            stamp(3);
+#pragma unroll
+            for (int j = 4; j < V; ++j) mfma_j(j);
+        }
         stamp(4);
         if constexpr (NP == 2) load_wk(tile_pass(t + 1), kb);
         if constexpr (kb == NK - 1) {

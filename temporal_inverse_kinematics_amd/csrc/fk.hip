@@ -312,8 +312,9 @@ hipError_t launch_fk_skin_sparse(const FkSkinSpArgs& a, hipStream_t st) {
         return hipErrorInvalidValue;
     constexpr int sbt = 4;   // bodies per tile (8: same time, more VGPRs)
     const int vt = (a.V + 255) / 256, nbt = (a.B + sbt - 1) / sbt;
-    // about 4 workgroups per CU, each walking a run of body tiles
-    int runs = (4 * (a.ncu > 0 ? a.ncu : 256) + vt - 1) / vt;
+    // about 16 workgroups per CU (3 resident at 134 VGPRs), each walking a run of body tiles:
+    // shorter runs than 4 per CU balance better (profiles/r06_ab_fk_landmarks_wpc.txt: -1 %)
+    int runs = (16 * (a.ncu > 0 ? a.ncu : 256) + vt - 1) / vt;
     runs = runs < nbt ? runs : nbt;
     (void)hipGetLastError();
     const dim3 grid(vt, runs);

@@ -12,13 +12,17 @@
 // more than one chunk (2048 bodies) run blend + skin per chunk, the chunks
 // alternating between the caller's stream and a handle-owned one, so one
 // chunk's HBM-bound skinning runs beside the next chunk's MFMA-bound blend
-// shapes (a 2048-body v_posed is 257 MB, about the Infinity Cache).
+// shapes (a 2048-body v_posed is 257 MB, about the Infinity Cache); each
+// chunk's landmarks follow its skinning in its stream.
 // TIK_FK_SKIN=dense: the skinning as a GEMM on the persistent xgemm kernel
 // (EPI_SKIN; also the path for weights with more than 16 live joints per
 // vertex). fp32: both GEMMs on cgemm.hip.
 // (Tried and not kept: the sparse skinning fused into the blend GEMM's
 // epilogue, v_posed never in HBM: bitwise equal but 1.31 vs 0.91 ms, the
-// per-tile A_j gather is latency-bound; profiles/r05_fk1_*.)
+// per-tile A_j gather is latency-bound; profiles/r05_fk1_*. Also the blends in
+// order on one stream with each chunk's skinning on the other: 1.01 vs 0.97 ms
+// per 4096 bodies, a lone 2048-body blend takes 0.37 ms and two concurrent
+// ones 0.56; profiles/r06_ab_fk_pipe.txt.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -355,6 +359,19 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         return TIK_OK;
     };
 
+    // the 21 vertex joints and 89 landmarks of bodies b0 .. b0 + n (after their vertices)
+    auto lmk = [&](int b0, int n, hipStream_t s) -> int {
+        tik::FkLmkArgs l{};
+        l.B = n; l.V = fk->V; l.njoints = fk->njoints; l.nextra = fk->nextra; l.nlmk = fk->nlmk; l.ndyn = fk->ndyn;
+        l.verts = vout + (size_t)b0 * V3; l.transl = transl ? transl + (size_t)b0 * 3 : nullptr;
+        l.extra = fk->extra.p; l.faces = fk->faces.p; l.lmk_faces = fk->lmk_faces.p;
+        l.lmk_bary = fk->lmk_bary.p; l.dyn_faces = fk->dyn_faces.p; l.dyn_bary = fk->dyn_bary.p;
+        l.dyn_bin = fk->dyn_bin.p + b0; l.joints = joints + (size_t)b0 * fk->njoints * 3;
+        ProfRange pr(pf, "fk_landmarks", 0.0, 4.0 * (double)n * (3.0 * 144 + 3.0 * 3 * 3 * 89), s);
+        HIP_TRY(tik::launch_fk_landmarks(l, s));
+        return TIK_OK;
+    };
+
     if (sparse) {
         const int CH = fk->chunk, nch = (B + CH - 1) / CH;
         if (nch > 1 && !fk->aux) {
@@ -371,7 +388,8 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
             hipStream_t s = (k & 1) ? fk->aux : st;
             // two v_posed chunk buffers, one per stream (reused in stream order)
             float* vp = fk->vposed.p + (size_t)(nch > 1 ? (k & 1) * CH : 0) * fk->ldv;
-            if ((rc = blend(b0, n, vp, s)) || (rc = skin(b0, n, vp, s))) return rc;
+            // each chunk's landmarks in its stream, beside the other stream's skinning
+            if ((rc = blend(b0, n, vp, s)) || (rc = skin(b0, n, vp, s)) || (rc = lmk(b0, n, s))) return rc;
         }
         if (nch > 1) {
             HIP_TRY(hipEventRecord(fk->ev_join, fk->aux));
@@ -411,15 +429,7 @@ int tik_fk_forward(tik_fk_t fk, const float* full_pose, const float* betas, cons
         HIP_TRY(tik::launch_cgemm(s, tik::CFG_S128x128, st, tik::PREC_F32));
     }
 
-    tik::FkLmkArgs l{};
-    l.B = B; l.V = fk->V; l.njoints = fk->njoints; l.nextra = fk->nextra; l.nlmk = fk->nlmk; l.ndyn = fk->ndyn;
-    l.verts = vout; l.transl = transl; l.extra = fk->extra.p; l.faces = fk->faces.p; l.lmk_faces = fk->lmk_faces.p;
-    l.lmk_bary = fk->lmk_bary.p; l.dyn_faces = fk->dyn_faces.p; l.dyn_bary = fk->dyn_bary.p;
-    l.dyn_bin = fk->dyn_bin.p; l.joints = joints;
-    {
-        ProfRange pr(pf, "fk_landmarks", 0.0, 4.0 * (double)B * (3.0 * 144 + 3.0 * 3 * 3 * 89), st);
-        HIP_TRY(tik::launch_fk_landmarks(l, st));
-    }
+    if (!sparse) return lmk(0, B, st);
     return TIK_OK;
 }
 

@@ -507,7 +507,10 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
 #pragma unroll
             for (int p = 0; p < 3; ++p) d[p] = *reinterpret_cast<const xbf16x8*>(P + xw_unit(2 * j + jb, fb + tap, p, g));
         };
-        auto mfma_n = [&](int n) __attribute__((always_inline)) {
+        // FG: the next tile's K blocks 0 and 1 are split / loaded in the gcn phase (its
+        // planes images are busy until then): K block 2 splits block 3 only, 3 nothing
+        constexpr bool SPL = !FG || kb < NKB - 1, LDN = !FG || kb < NKB - 2;
+        auto mfma_n = [&](int n, int unit) __attribute__((always_inline)) {
             if (n + XPF < NI) rd(n + XPF, xr[(n + XPF) % (XPF + 1)]);
             __builtin_amdgcn_sched_barrier(0);
             if (XW_OFF(4)) return;
@@ -524,6 +527,17 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
                 acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[1], x[0], acc[j][cb], 0, 0, 0);
                 acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wk[0], x[0], acc[j][cb], 0, 0, 0);
             }
+            if (unit >= 0) {
+                // a split unit after the item's MFMAs in program order, its VALU then
+                // scheduled between them (its LDS writes and load anywhere)
+                if (!XW_OFF(2)) split_unit(kb + 1, rb[nb], unit);
+                if (LDN) load_unit(s + 1 + D, rb[nb], unit);
+#pragma unroll
+                for (int q = 0; q < 6 * CB; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
         };
 #pragma unroll
@@ -532,20 +546,15 @@ __global__ __launch_bounds__(64 * NW, 1) void xtws_kernel(XTConvArgs a) {
         // MFMA items (waves leave the barrier together: a split in one piece would
         // idle the MFMA pipe), each unit's register slot reloaded right after (past
         // the run: zeros, never read)
-        // FG: the next tile's K blocks 0 and 1 are split / loaded in the gcn phase (its
-        // planes images are busy until then): K block 2 splits block 3 only, 3 nothing
-        constexpr bool SPL = !FG || kb < NKB - 1, LDN = !FG || kb < NKB - 2;
 #pragma unroll
         for (int n = 0; n < NI; ++n) {
-            mfma_n(n);
+            int unit = -1;
 #pragma unroll
             for (int i = 0; i < NLD; ++i)
                 // FG K block 0: its rb was loaded just before the tile, so its split units go late
-                if (SPL && n == (FG && kb == 0 ? NI / 2 + (i * NI) / (2 * NLD) : XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD))) {
-                    if (!XW_OFF(2)) split_unit(kb + 1, rb[nb], i);
-                    if (LDN) load_unit(s + 1 + D, rb[nb], i);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+                if (SPL && n == (FG && kb == 0 ? NI / 2 + (i * NI) / (2 * NLD) : XW_SPLIT_AT ? i * NI / NLD + 1 : ((2 * i + 1) * NI) / (2 * NLD)) + 1)
+                    unit = i;
+            mfma_n(n, unit);
         }
         if constexpr (kb == NKB - 1) {
             // ---- epilogue: (acc + x) + bias, ReLU. The identity DMA of this tile was issued

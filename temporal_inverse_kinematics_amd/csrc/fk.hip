@@ -253,7 +253,11 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
 #pragma unroll
         for (int b = 0; b < SBT; ++b) {
             const int body = min(t * SBT + b, a.B - 1);
-            __builtin_memcpy(&pv[b][0], a.vposed + (size_t)body * a.ldv + 3 * vc, 12);
+            // streaming (nt) loads: v_posed is read once
+            const float* q = a.vposed + (size_t)body * a.ldv + 3 * vc;
+            pv[b][0] = __builtin_nontemporal_load(q);
+            pv[b][1] = __builtin_nontemporal_load(q + 1);
+            pv[b][2] = __builtin_nontemporal_load(q + 2);
         }
     };
     auto put = [&](int buf) __attribute__((always_inline)) {
@@ -289,7 +293,12 @@ __global__ __launch_bounds__(256) void fk_skin_sparse_kernel(FkSkinSpArgs a, int
             for (int g = 0; g < 3; ++g)
                 o[g] = fmaf(T[4 * g], cv[b][0], fmaf(T[4 * g + 1], cv[b][1], fmaf(T[4 * g + 2], cv[b][2], T[4 * g + 3]))) +
                        a.transl[bc * 3 + g];
-            if (vok && body < a.B) __builtin_memcpy(a.verts + (size_t)body * 3 * a.V + 3 * v, o, 12);
+            if (vok && body < a.B) {   // streaming (nt) stores: -4 % skinning (profiles/r06_ab_fk_nontemporal.txt)
+                float* d = a.verts + (size_t)body * 3 * a.V + 3 * v;
+                __builtin_nontemporal_store(o[0], d);
+                __builtin_nontemporal_store(o[1], d + 1);
+                __builtin_nontemporal_store(o[2], d + 2);
+            }
             __builtin_amdgcn_sched_barrier(0);   // one body's LDS reads in flight at a time (registers)
         }
         if (t + 1 < t1) put((t + 1) & 1);

@@ -106,7 +106,8 @@ __global__ __launch_bounds__(512, 1) void xgraph_kernel(XGraphArgs a) {
         const int U = 512 * i + tid, m = U >> 3, u = U & 7;
         const int q = q0 + m / V;
         const unsigned off = live && U < NU && q < QO && !XG_OFF(1) ? (unsigned)(((long long)q0 * V + m) * a.ldx * 4 + kb * 128 + u * 16) : DMA_OOB;
-        r[i] = tik_llvm_raw_buffer_load_v4f32(rX, (int)off, 0, 0);
+        // nontemporal (aux 2: nt): XGW.L2 -3.5 %, the others within noise (profiles/r06_ab_xgraph_nt_loads2.txt)
+        r[i] = tik_llvm_raw_buffer_load_v4f32(rX, (int)off, 0, 2);
     };
     auto load = [&](int s, f32x4 (&r)[NLD]) __attribute__((always_inline)) {
 #pragma unroll

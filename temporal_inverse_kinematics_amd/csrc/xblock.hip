@@ -155,7 +155,8 @@ __global__ __launch_bounds__(512, 1) void xblock_kernel(XBlkArgs a) {
             const int q = q0 - 1 + (int)((c >> 24) & 0x7F);
             const bool ok = !(c >> 31) && q >= 0 && q < QO;
             const unsigned off = ok ? (unsigned)((long long)(q0 - 1) * V * ROWB) + (c & 0xFFFFFFu) : DMA_OOB;
-            dma16(rX, ximg + ins * 1024, off, 0);
+            // nt cache policy (aux 2): XB1 -1.6 % (profiles/r06_ab_xblock_nt_dma.txt)
+            tik_llvm_raw_buffer_load_lds(rX, (__attribute__((address_space(3))) unsigned*)(ximg + ins * 1024), 16, (int)off, 0, 0, 2);
         }
     };
     // ---- block 0: raw keypoints of a tile, loaded a tile ahead into registers
